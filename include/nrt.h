@@ -1,0 +1,196 @@
+/*
+ * nrt.h — C ABI of the MI355X-native renderer for nr-ray-tracer's per-pixel
+ * path-tracing loop.
+ *
+ * The reference has no FFI: the path sits behind Rust generics/traits
+ * (SURVEY.md §8b).  Each entry point below names the reference interface it
+ * replaces; a Rust host binds them with one `extern "C"` block
+ * (INTEGRATION.md).  Conventions:
+ *   - every int-returning call returns NRT_OK (0) or a negative NRT_E_* code and
+ *     never aborts the process; nrt_last_error() gives the message (thread-local);
+ *   - the caller owns every buffer it passes; the library copies all inputs;
+ *   - all structs are plain data; no torch / HIP types appear in signatures
+ *     (streams are passed as void*).
+ */
+#ifndef NRT_H
+#define NRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NRT_ABI_VERSION 1
+
+enum {
+    NRT_OK = 0,
+    NRT_E_INVALID = -1,     /* bad argument */
+    NRT_E_LOAD = -2,        /* scene file / config error (anyhow::Error in the reference) */
+    NRT_E_DEVICE = -3,      /* HIP error / no device */
+    NRT_E_UNSUPPORTED = -4  /* feature outside the accelerated path (e.g. Perlin textures) */
+};
+
+enum nrt_precision { NRT_PRECISION_F64 = 0, NRT_PRECISION_F32 = 1 };
+enum nrt_rng { NRT_RNG_CHACHA8 = 0, NRT_RNG_PHILOX = 1 };
+
+typedef struct nrt_scene nrt_scene;
+typedef struct nrt_builder nrt_builder;
+
+/* CameraConfig (packages/ray-tracer/src/cli.rs:157-270): each field optional,
+ * present when its NRT_CC_* bit is set in `set`.  Angles in degrees. */
+enum {
+    NRT_CC_WIDTH = 1u << 0,
+    NRT_CC_HEIGHT = 1u << 1,
+    NRT_CC_ASPECT_RATIO = 1u << 2,
+    NRT_CC_BACKGROUND_COLOR = 1u << 3,
+    NRT_CC_LOOK_AT = 1u << 4,
+    NRT_CC_LOOK_FROM = 1u << 5,
+    NRT_CC_VIEW_UP = 1u << 6,
+    NRT_CC_FOCAL_LENGTH = 1u << 7,
+    NRT_CC_FIELD_OF_VIEW = 1u << 8,
+    NRT_CC_DEFOCUS_ANGLE = 1u << 9,
+    NRT_CC_FOCUS_DISTANCE = 1u << 10,
+    NRT_CC_SAMPLES_PER_PIXEL = 1u << 11,
+    NRT_CC_RAY_MAX_BOUNCES = 1u << 12
+};
+
+typedef struct {
+    uint32_t set;
+    uint32_t reserved;
+    uint64_t width, height;
+    double aspect_ratio;
+    double background_color[3];
+    double look_at[3];
+    double look_from[3];
+    double view_up[3];
+    double focal_length; /* parsed, ignored — as in the reference (cli.rs:229) */
+    double field_of_view;
+    double defocus_angle;
+    double focus_distance;
+    uint64_t samples_per_pixel;
+    uint64_t ray_max_bounces;
+} nrt_camera_config;
+
+/* CameraBuilder (lib/camera.rs:30-41); angles in radians. */
+typedef struct {
+    uint64_t width, height;
+    double background_color[3];
+    double look_from[3];
+    double look_at[3];
+    double view_up[3];
+    double defocus_angle;
+    double focus_dist;
+    double field_of_view;
+    uint64_t ray_max_bounces;
+    uint64_t samples_per_pixel;
+} nrt_camera_builder;
+
+/* Camera after CameraBuilder::build (lib/camera.rs:205-227). */
+typedef struct {
+    uint64_t width, height;
+    uint64_t samples_per_pixel;
+    uint64_t ray_max_bounces;
+    double background_color[3];
+    double look_from[3];
+    double defocus_disk_u[3];
+    double defocus_disk_v[3];
+    double pixel_delta_u[3];
+    double pixel_delta_v[3];
+    double top_left[3];
+} nrt_camera;
+
+typedef struct {
+    uint32_t precision;  /* nrt_precision */
+    uint32_t rng;        /* nrt_rng */
+    int32_t device;      /* HIP device ordinal; -1 = current device */
+    uint32_t row_offset; /* render image rows y = row_offset + k*row_stride ... */
+    uint32_t row_stride; /* ... (0 or 1: every row); output rows are compact */
+    uint32_t reserved[3];
+} nrt_render_opts;
+
+typedef struct {
+    uint64_t nodes, prims, instances, xforms, materials, textures, texels;
+    uint32_t trees, max_instance_depth;
+    uint64_t device_bytes; /* HBM bytes of the flattened scene on one device */
+} nrt_scene_stats;
+
+typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);
+
+/* ---- library ---------------------------------------------------------- */
+int nrt_abi_version(void);
+const char* nrt_last_error(void);   /* thread-local; message text mirrors anyhow's */
+int nrt_device_count(void);
+
+/* ---- camera (lib/camera.rs:162-203, 94-159; app cli.rs:316-402) --------- */
+void nrt_camera_builder_default(nrt_camera_builder* out);           /* CameraBuilder::default */
+int nrt_camera_build(const nrt_camera_builder* b, nrt_camera* out);  /* CameraBuilder::build */
+/* CameraConfig::try_update onto a builder (image-size rules, degrees->radians) */
+int nrt_camera_config_apply(const nrt_camera_config* cfg, nrt_camera_builder* b);
+
+/* ---- scene from file: SceneConfig::try_load_scene + merge_with + try_build
+ *      (app scene_config.rs:475-496, render.rs:556-560).  Relative paths inside
+ *      the file (nested scenes, textures) resolve against the process CWD, as in
+ *      the reference.  `overrides` may be NULL. */
+int nrt_scene_load(const char* path, const nrt_camera_config* overrides, nrt_scene** out, nrt_camera* camera);
+
+/* ---- scene from the library constructors (the Hitable/Material/Texture
+ *      trait surface of nr-ray-tracer-lib).  Handles are small non-negative
+ *      integers (negative = error). */
+nrt_builder* nrt_builder_new(void);
+void nrt_builder_free(nrt_builder* b);
+int32_t nrt_texture_solid(nrt_builder* b, const double color[3]);                      /* SolidColor::new */
+int32_t nrt_texture_image(nrt_builder* b, uint32_t w, uint32_t h, const float* rgb);   /* Image (Rgb32F texels) */
+int32_t nrt_texture_image_file(nrt_builder* b, const char* path);                      /* Image::try_from_path */
+int32_t nrt_texture_checker(nrt_builder* b, int32_t even, int32_t odd, double scale);  /* CheckerBuilder */
+int32_t nrt_material_lambertian(nrt_builder* b, int32_t texture);                       /* Lambertian::with_texture */
+int32_t nrt_material_metal(nrt_builder* b, double fuzz, int32_t texture);               /* MetalBuilder */
+int32_t nrt_material_dielectric(nrt_builder* b, double refraction_index);               /* Dielectric::new */
+int32_t nrt_material_diffuse_light(nrt_builder* b, double intensity, int32_t texture);  /* DiffuseLightBuilder */
+int32_t nrt_object_sphere(nrt_builder* b, const double center[3], double radius, int32_t material); /* SphereBuilder */
+int32_t nrt_object_quad(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material);
+int32_t nrt_object_triangle(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material);
+int32_t nrt_object_bvh(nrt_builder* b, const int32_t* objects, size_t count);          /* BVH::from */
+int32_t nrt_object_translate(nrt_builder* b, int32_t object, const double offset[3]);  /* Translate::new */
+int32_t nrt_object_rotate_x(nrt_builder* b, int32_t object, double angle);             /* Rotate::axis_x */
+int32_t nrt_object_rotate_y(nrt_builder* b, int32_t object, double angle);             /* Rotate::axis_y */
+int32_t nrt_object_rotate_z(nrt_builder* b, int32_t object, double angle);             /* Rotate::axis_z */
+int32_t nrt_object_scale(nrt_builder* b, int32_t object, const double scale[3]);       /* Scale::new */
+/* Scene { objects: BVH } (lib/scene.rs:6-10); `bvh` must come from nrt_object_bvh. */
+int nrt_builder_finish(nrt_builder* b, int32_t bvh, nrt_scene** out);
+
+/* ---- render: Scene::render / Camera::render (lib/scene.rs:13-18, lib/camera.rs:302-343)
+ * out_rgb: caller-owned, rows*width*3 f32, row-major (Rgb32FImage layout), where
+ * rows = the rows selected by opts (all rows by default).  Synchronous.
+ * progress (may be NULL) is called from the calling thread with the number of
+ * pixels finished so far, at launch granularity. */
+int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts, float* out_rgb,
+               size_t out_len, nrt_progress_fn progress, void* user);
+/* Same, into device memory on `hip_stream` (hipStream_t, NULL = default stream);
+ * asynchronous: returns after enqueueing. */
+int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
+                      float* dev_out_rgb, size_t out_len, void* hip_stream);
+/* Number of rows selected by opts for an image of `height` rows. */
+uint32_t nrt_rows_selected(uint32_t height, const nrt_render_opts* opts);
+/* Upload the flattened scene to `device` now (otherwise done on first render). */
+int nrt_scene_upload(nrt_scene* scene, int32_t device);
+
+int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out);
+/* Canonical text dump of the scene graph (BVH, boxes, transforms, materials) in
+ * hex floats; *needed = bytes incl. NUL.  Used by parity tests. */
+int nrt_scene_dump(const nrt_scene* scene, char* buf, size_t cap, size_t* needed);
+void nrt_scene_destroy(nrt_scene* scene);
+
+/* gamma_correction + to_rgb8 (lib/image.rs:53-57; image crate Rgb32F->Rgb8). */
+int nrt_image_to_rgb8(const float* rgb, size_t n_floats, float gamma, uint8_t* out);
+
+/* Tests: first `count` next_u64 draws of `lanes` consecutive pixel streams
+ * (ChaCha8: stream = pixel index; Philox: counter (pixel, sample, pair)). */
+int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NRT_H */

@@ -1,0 +1,480 @@
+// C ABI (include/nrt.h).  Every entry point converts exceptions into status
+// codes + a thread-local message; nothing here aborts the process.
+#include "../../include/nrt.h"
+
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "flatten.hpp"
+#include "gpu.hpp"
+#include "scene.hpp"
+#include "scene_config.hpp"
+
+using namespace nrt;
+
+struct nrt_scene {
+    ObjectPtr graph;     // Scene.objects (top-level BVH)
+    FlatScene flat;
+    std::mutex mu;
+    std::vector<DeviceScene*> per_device;  // index = HIP ordinal
+    ~nrt_scene() {
+        for (DeviceScene* d : per_device) gpu_free_scene(d);
+    }
+};
+
+struct nrt_builder {
+    std::vector<TexturePtr> textures;
+    std::vector<MaterialPtr> materials;
+    std::vector<ObjectPtr> objects;
+};
+
+int nrt_current_device();  // render.hip
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct UnsupportedError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+int set_error(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+template <class F>
+int guarded(int fail_code, F&& f) {
+    try {
+        g_last_error.clear();
+        return f();
+    } catch (const ParseError& e) {
+        return set_error(NRT_E_LOAD, e.what());
+    } catch (const std::bad_alloc&) {
+        return set_error(NRT_E_DEVICE, "out of memory");
+    } catch (const std::exception& e) {
+        std::string m = e.what();
+        if (m.find("outside the accelerated path") != std::string::npos) return set_error(NRT_E_UNSUPPORTED, m);
+        if (m.rfind("HIP error", 0) == 0) return set_error(NRT_E_DEVICE, m);
+        return set_error(fail_code, m);
+    } catch (...) {
+        return set_error(fail_code, "unknown error");
+    }
+}
+
+V3 v3of(const double* d) { return v3(d[0], d[1], d[2]); }
+void put3(double* d, V3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; }
+
+CameraBuilder from_c(const nrt_camera_builder& b) {
+    CameraBuilder c;
+    c.width = b.width;
+    c.height = b.height;
+    c.background_color = v3of(b.background_color);
+    c.look_from = v3of(b.look_from);
+    c.look_at = v3of(b.look_at);
+    c.view_up = v3of(b.view_up);
+    c.defocus_angle = b.defocus_angle;
+    c.focus_dist = b.focus_dist;
+    c.field_of_view = b.field_of_view;
+    c.ray_max_bounces = b.ray_max_bounces;
+    c.samples_per_pixel = b.samples_per_pixel;
+    return c;
+}
+void to_c(const CameraBuilder& c, nrt_camera_builder* b) {
+    b->width = c.width;
+    b->height = c.height;
+    put3(b->background_color, c.background_color);
+    put3(b->look_from, c.look_from);
+    put3(b->look_at, c.look_at);
+    put3(b->view_up, c.view_up);
+    b->defocus_angle = c.defocus_angle;
+    b->focus_dist = c.focus_dist;
+    b->field_of_view = c.field_of_view;
+    b->ray_max_bounces = c.ray_max_bounces;
+    b->samples_per_pixel = c.samples_per_pixel;
+}
+void to_c(const Camera& c, nrt_camera* o) {
+    o->width = c.width;
+    o->height = c.height;
+    o->samples_per_pixel = c.samples_per_pixel;
+    o->ray_max_bounces = c.ray_max_bounces;
+    put3(o->background_color, c.background_color);
+    put3(o->look_from, c.look_from);
+    put3(o->defocus_disk_u, c.defocus_disk_u);
+    put3(o->defocus_disk_v, c.defocus_disk_v);
+    put3(o->pixel_delta_u, c.pixel_delta_u);
+    put3(o->pixel_delta_v, c.pixel_delta_v);
+    put3(o->top_left, c.top_left);
+}
+
+CameraConfig from_c(const nrt_camera_config& c) {
+    CameraConfig o;
+    const uint32_t s = c.set;
+    if (s & NRT_CC_WIDTH) { o.has_width = true; o.width = c.width; }
+    if (s & NRT_CC_HEIGHT) { o.has_height = true; o.height = c.height; }
+    if (s & NRT_CC_ASPECT_RATIO) { o.has_aspect_ratio = true; o.aspect_ratio = c.aspect_ratio; }
+    if (s & NRT_CC_BACKGROUND_COLOR) { o.has_background_color = true; o.background_color = v3of(c.background_color); }
+    if (s & NRT_CC_LOOK_AT) { o.has_look_at = true; o.look_at = v3of(c.look_at); }
+    if (s & NRT_CC_LOOK_FROM) { o.has_look_from = true; o.look_from = v3of(c.look_from); }
+    if (s & NRT_CC_VIEW_UP) { o.has_view_up = true; o.view_up = v3of(c.view_up); }
+    if (s & NRT_CC_FOCAL_LENGTH) { o.has_focal_length = true; o.focal_length = c.focal_length; }
+    if (s & NRT_CC_FIELD_OF_VIEW) { o.has_field_of_view = true; o.field_of_view = c.field_of_view; }
+    if (s & NRT_CC_DEFOCUS_ANGLE) { o.has_defocus_angle = true; o.defocus_angle = c.defocus_angle; }
+    if (s & NRT_CC_FOCUS_DISTANCE) { o.has_focus_distance = true; o.focus_distance = c.focus_distance; }
+    if (s & NRT_CC_SAMPLES_PER_PIXEL) { o.has_samples_per_pixel = true; o.samples_per_pixel = c.samples_per_pixel; }
+    if (s & NRT_CC_RAY_MAX_BOUNCES) { o.has_ray_max_bounces = true; o.ray_max_bounces = c.ray_max_bounces; }
+    return o;
+}
+
+uint32_t rows_selected(uint32_t height, const nrt_render_opts* o) {
+    const uint32_t off = o ? o->row_offset : 0;
+    const uint32_t stride = (o && o->row_stride > 1) ? o->row_stride : 1;
+    if (off >= height) return 0;
+    return (height - off + stride - 1) / stride;
+}
+
+DeviceScene* device_scene(nrt_scene* s, int device) {
+    std::lock_guard<std::mutex> lock(s->mu);
+    if ((int)s->per_device.size() <= device) s->per_device.resize((size_t)device + 1, nullptr);
+    if (!s->per_device[(size_t)device]) s->per_device[(size_t)device] = gpu_upload_scene(s->flat, device);
+    return s->per_device[(size_t)device];
+}
+
+int resolve_device(const nrt_render_opts* o) {
+    int n = gpu_device_count();
+    if (n <= 0) throw std::runtime_error("HIP error in device query: no GPU device available");
+    int dev = o ? o->device : -1;
+    if (dev < 0) {
+        dev = nrt_current_device();
+    }
+    if (dev >= n) throw std::invalid_argument("device ordinal out of range");
+    return dev;
+}
+
+RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t rows) {
+    if (c.width == 0 || c.height == 0) throw std::invalid_argument("image width and height must be > 0");
+    if (c.width * c.height > 0xFFFFFFFFull) throw std::invalid_argument("image has more than 2^32 pixels");
+    if (c.samples_per_pixel > 0xFFFFFFFFull || c.ray_max_bounces > 0xFFFFFFFFull)
+        throw std::invalid_argument("samples_per_pixel / ray_max_bounces exceed 2^32-1");
+    RenderParams p{};
+    for (int k = 0; k < 3; ++k) {
+        p.top_left[k] = c.top_left[k];
+        p.pixel_delta_u[k] = c.pixel_delta_u[k];
+        p.pixel_delta_v[k] = c.pixel_delta_v[k];
+        p.look_from[k] = c.look_from[k];
+        p.defocus_disk_u[k] = c.defocus_disk_u[k];
+        p.defocus_disk_v[k] = c.defocus_disk_v[k];
+        p.background[k] = c.background_color[k];
+    }
+    p.width = (uint32_t)c.width;
+    p.height = (uint32_t)c.height;
+    p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;
+    p.max_bounces = (uint32_t)c.ray_max_bounces;
+    p.row_offset = o ? o->row_offset : 0;
+    p.row_stride = (o && o->row_stride > 1) ? o->row_stride : 1;
+    p.rows = rows;
+    p.pixel_begin = 0;
+    p.pixel_end = rows * p.width;
+    return p;
+}
+
+void check_opts(const nrt_render_opts* o) {
+    if (!o) return;
+    if (o->precision > NRT_PRECISION_F32) throw std::invalid_argument("unknown precision");
+    if (o->rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
+}
+
+}  // namespace
+
+// device helpers implemented in device_util.hip
+extern "C++" {
+namespace nrt {
+void* device_alloc(size_t bytes, int device);
+void device_free(void* p, int device);
+void device_copy_to_host(void* dst, const void* src, size_t bytes, int device);
+void device_sync(int device);
+}
+}
+
+extern "C" {
+
+int nrt_abi_version(void) { return NRT_ABI_VERSION; }
+const char* nrt_last_error(void) { return g_last_error.c_str(); }
+int nrt_device_count(void) { return gpu_device_count(); }
+
+void nrt_camera_builder_default(nrt_camera_builder* out) {
+    if (out) to_c(CameraBuilder{}, out);
+}
+
+int nrt_camera_build(const nrt_camera_builder* b, nrt_camera* out) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!b || !out) throw std::invalid_argument("null argument");
+        to_c(camera_build(from_c(*b)), out);
+        return NRT_OK;
+    });
+}
+
+int nrt_camera_config_apply(const nrt_camera_config* cfg, nrt_camera_builder* b) {
+    return guarded(NRT_E_LOAD, [&]() {
+        if (!cfg || !b) throw std::invalid_argument("null argument");
+        CameraBuilder cb = from_c(*b);
+        from_c(*cfg).try_update(cb);
+        to_c(cb, b);
+        return NRT_OK;
+    });
+}
+
+int nrt_scene_load(const char* path, const nrt_camera_config* overrides, nrt_scene** out, nrt_camera* camera) {
+    if (out) *out = nullptr;
+    return guarded(NRT_E_LOAD, [&]() {
+        if (!path || !out) throw std::invalid_argument("null argument");
+        CameraConfig cli;
+        if (overrides) cli = from_c(*overrides);
+        LoadedScene ls = load_scene_file(path, overrides ? &cli : nullptr);
+        auto s = std::make_unique<nrt_scene>();
+        s->graph = ls.objects;
+        s->flat = flatten_scene(ls.objects);
+        if (camera) to_c(ls.camera, camera);
+        *out = s.release();
+        return NRT_OK;
+    });
+}
+
+nrt_builder* nrt_builder_new(void) { return new (std::nothrow) nrt_builder(); }
+void nrt_builder_free(nrt_builder* b) { delete b; }
+
+static int32_t add_tex(nrt_builder* b, TexturePtr t) {
+    b->textures.push_back(std::move(t));
+    return (int32_t)b->textures.size() - 1;
+}
+static int32_t add_mat(nrt_builder* b, MaterialPtr m) {
+    b->materials.push_back(std::move(m));
+    return (int32_t)b->materials.size() - 1;
+}
+static int32_t add_obj(nrt_builder* b, ObjectPtr o) {
+    b->objects.push_back(std::move(o));
+    return (int32_t)b->objects.size() - 1;
+}
+static TexturePtr tex_at(nrt_builder* b, int32_t id) {
+    if (id < 0 || (size_t)id >= b->textures.size()) throw std::invalid_argument("invalid texture handle");
+    return b->textures[(size_t)id];
+}
+static MaterialPtr mat_at(nrt_builder* b, int32_t id) {
+    if (id < 0 || (size_t)id >= b->materials.size()) throw std::invalid_argument("invalid material handle");
+    return b->materials[(size_t)id];
+}
+static ObjectPtr obj_at(nrt_builder* b, int32_t id) {
+    if (id < 0 || (size_t)id >= b->objects.size()) throw std::invalid_argument("invalid object handle");
+    return b->objects[(size_t)id];
+}
+
+#define NRT_BUILD(body)                                                   \
+    if (!b) return set_error(NRT_E_INVALID, "null builder");               \
+    return guarded(NRT_E_INVALID, [&]() -> int { body });
+
+int32_t nrt_texture_solid(nrt_builder* b, const double color[3]) {
+    NRT_BUILD(auto t = std::make_shared<Texture>(); t->kind = Texture::Solid; t->color = v3of(color);
+              return add_tex(b, t);)
+}
+int32_t nrt_texture_image(nrt_builder* b, uint32_t w, uint32_t h, const float* rgb) {
+    NRT_BUILD(if (!rgb || w == 0 || h == 0) throw std::invalid_argument("empty image");
+              auto t = std::make_shared<Texture>(); t->kind = Texture::Image; t->width = w; t->height = h;
+              t->texels = std::make_shared<std::vector<float>>(rgb, rgb + 3ull * w * h); return add_tex(b, t);)
+}
+int32_t nrt_texture_image_file(nrt_builder* b, const char* path) {
+    NRT_BUILD(if (!path) throw std::invalid_argument("null path"); DecodedImage img = decode_image_file(path);
+              auto t = std::make_shared<Texture>(); t->kind = Texture::Image; t->width = img.width;
+              t->height = img.height; t->texels = std::make_shared<std::vector<float>>(std::move(img.rgb));
+              return add_tex(b, t);)
+}
+int32_t nrt_texture_checker(nrt_builder* b, int32_t even, int32_t odd, double scale) {
+    NRT_BUILD(auto t = std::make_shared<Texture>(); t->kind = Texture::Checker; t->even = tex_at(b, even);
+              t->odd = tex_at(b, odd); t->scale = scale; return add_tex(b, t);)
+}
+int32_t nrt_material_lambertian(nrt_builder* b, int32_t texture) {
+    NRT_BUILD(auto m = std::make_shared<Material>(); m->kind = Material::Lambertian; m->texture = tex_at(b, texture);
+              return add_mat(b, m);)
+}
+int32_t nrt_material_metal(nrt_builder* b, double fuzz, int32_t texture) {
+    NRT_BUILD(auto m = std::make_shared<Material>(); m->kind = Material::Metal; m->fuzz = fuzz;
+              m->texture = tex_at(b, texture); return add_mat(b, m);)
+}
+int32_t nrt_material_dielectric(nrt_builder* b, double refraction_index) {
+    NRT_BUILD(auto m = std::make_shared<Material>(); m->kind = Material::Dielectric;
+              m->refraction_index = refraction_index; return add_mat(b, m);)
+}
+int32_t nrt_material_diffuse_light(nrt_builder* b, double intensity, int32_t texture) {
+    NRT_BUILD(auto m = std::make_shared<Material>(); m->kind = Material::DiffuseLight; m->intensity = intensity;
+              m->texture = tex_at(b, texture); return add_mat(b, m);)
+}
+int32_t nrt_object_sphere(nrt_builder* b, const double center[3], double radius, int32_t material) {
+    NRT_BUILD(return add_obj(b, make_sphere(v3of(center), radius, mat_at(b, material)));)
+}
+int32_t nrt_object_quad(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material) {
+    NRT_BUILD(return add_obj(b, make_plane(Object::Quad, v3of(p), v3of(u), v3of(v), mat_at(b, material)));)
+}
+int32_t nrt_object_triangle(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material) {
+    NRT_BUILD(return add_obj(b, make_plane(Object::Triangle, v3of(p), v3of(u), v3of(v), mat_at(b, material)));)
+}
+int32_t nrt_object_bvh(nrt_builder* b, const int32_t* objects, size_t count) {
+    NRT_BUILD(if (count && !objects) throw std::invalid_argument("null object list"); std::vector<ObjectPtr> list;
+              for (size_t k = 0; k < count; ++k) list.push_back(obj_at(b, objects[k]));
+              return add_obj(b, make_bvh(list));)
+}
+int32_t nrt_object_translate(nrt_builder* b, int32_t object, const double offset[3]) {
+    NRT_BUILD(return add_obj(b, make_translate(obj_at(b, object), v3of(offset)));)
+}
+int32_t nrt_object_rotate_x(nrt_builder* b, int32_t object, double angle) {
+    NRT_BUILD(return add_obj(b, make_rotate(obj_at(b, object), v3(1, 0, 0), angle));)
+}
+int32_t nrt_object_rotate_y(nrt_builder* b, int32_t object, double angle) {
+    NRT_BUILD(return add_obj(b, make_rotate(obj_at(b, object), v3(0, 1, 0), angle));)
+}
+int32_t nrt_object_rotate_z(nrt_builder* b, int32_t object, double angle) {
+    NRT_BUILD(return add_obj(b, make_rotate(obj_at(b, object), v3(0, 0, 1), angle));)
+}
+int32_t nrt_object_scale(nrt_builder* b, int32_t object, const double scale[3]) {
+    NRT_BUILD(return add_obj(b, make_scale(obj_at(b, object), v3of(scale)));)
+}
+
+int nrt_builder_finish(nrt_builder* b, int32_t bvh, nrt_scene** out) {
+    if (out) *out = nullptr;
+    NRT_BUILD(if (!out) throw std::invalid_argument("null output"); ObjectPtr root = obj_at(b, bvh);
+              if (root->kind != Object::BvhNode && root->kind != Object::BvhLeaf && root->kind != Object::BvhEmpty)
+                  throw std::invalid_argument("scene root must be a BVH (nrt_object_bvh)");
+              auto s = std::make_unique<nrt_scene>(); s->graph = root; s->flat = flatten_scene(root);
+              *out = s.release(); return NRT_OK;)
+}
+
+uint32_t nrt_rows_selected(uint32_t height, const nrt_render_opts* opts) { return rows_selected(height, opts); }
+
+int nrt_scene_upload(nrt_scene* scene, int32_t device) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!scene) throw std::invalid_argument("null scene");
+        nrt_render_opts o{};
+        o.device = device;
+        device_scene(scene, resolve_device(&o));
+        return NRT_OK;
+    });
+}
+
+int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
+                      float* dev_out_rgb, size_t out_len, void* hip_stream) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!scene || !camera || !dev_out_rgb) throw std::invalid_argument("null argument");
+        check_opts(opts);
+        const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
+        RenderParams p = make_params(*camera, opts, rows);
+        if (out_len < (size_t)rows * p.width * 3) throw std::invalid_argument("output buffer too small");
+        const int dev = resolve_device(opts);
+        DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
+        p.out = dev_out_rgb;
+        gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, hip_stream);
+        return NRT_OK;
+    });
+}
+
+int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts, float* out_rgb,
+               size_t out_len, nrt_progress_fn progress, void* user) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!scene || !camera || !out_rgb) throw std::invalid_argument("null argument");
+        check_opts(opts);
+        const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
+        RenderParams p = make_params(*camera, opts, rows);
+        const size_t n = (size_t)rows * p.width * 3;
+        if (out_len < n) throw std::invalid_argument("output buffer too small");
+        if (n == 0) return NRT_OK;
+        const int dev = resolve_device(opts);
+        DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
+        void* d = device_alloc(n * sizeof(float), dev);
+        try {
+            p.out = (float*)d;
+            const uint32_t total = p.pixel_end;
+            const uint32_t chunks = progress ? 16u : 1u;
+            const uint32_t per = (total + chunks - 1) / chunks;
+            for (uint32_t c = 0; c < chunks; ++c) {
+                p.pixel_begin = c * per;
+                p.pixel_end = std::min(total, (c + 1) * per);
+                if (p.pixel_begin >= p.pixel_end) break;
+                gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, nullptr);
+                if (progress) {
+                    device_sync(dev);
+                    progress(user, p.pixel_end);
+                }
+            }
+            device_sync(dev);
+            device_copy_to_host(out_rgb, d, n * sizeof(float), dev);
+        } catch (...) {
+            device_free(d, dev);
+            throw;
+        }
+        device_free(d, dev);
+        return NRT_OK;
+    });
+}
+
+int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!scene || !out) throw std::invalid_argument("null argument");
+        const FlatScene& f = scene->flat;
+        out->nodes = f.nodes.size();
+        out->prims = f.prims.size();
+        out->instances = f.instances.size();
+        out->xforms = f.xforms.size();
+        out->materials = f.materials.size();
+        out->textures = f.textures.size();
+        out->texels = f.texels.size() / 3;
+        out->trees = f.num_trees;
+        out->max_instance_depth = (uint32_t)f.max_depth;
+        out->device_bytes = f.nodes.size() * (sizeof(DNode<double>) + sizeof(DNode<float>)) +
+                            f.prims.size() * (sizeof(DPrim<double>) + sizeof(DPrim<float>)) +
+                            f.xforms.size() * (sizeof(DXform<double>) + sizeof(DXform<float>)) +
+                            f.instances.size() * sizeof(DInstance) + f.materials.size() * sizeof(DMaterial) +
+                            f.textures.size() * sizeof(DTexture) + f.texels.size() * sizeof(float);
+        return NRT_OK;
+    });
+}
+
+int nrt_scene_dump(const nrt_scene* scene, char* buf, size_t cap, size_t* needed) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!scene) throw std::invalid_argument("null scene");
+        const std::string s = dump_graph(scene->graph);
+        if (needed) *needed = s.size() + 1;
+        if (buf && cap) {
+            const size_t n = std::min(cap - 1, s.size());
+            std::memcpy(buf, s.data(), n);
+            buf[n] = '\0';
+        }
+        return NRT_OK;
+    });
+}
+
+void nrt_scene_destroy(nrt_scene* scene) { delete scene; }
+
+int nrt_image_to_rgb8(const float* rgb, size_t n, float gamma, uint8_t* out) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if ((n && !rgb) || (n && !out)) throw std::invalid_argument("null argument");
+        for (size_t k = 0; k < n; ++k) {
+            const float g = std::pow(rgb[k], gamma);           // gamma_correction: p.powf(gamma)
+            const float c = !(g < 1.0f) ? 1.0f : std::fmax(g, 0.0f);  // image crate normalize_float
+            out[k] = (uint8_t)std::nearbyint(std::round(c * 255.0f));
+        }
+        return NRT_OK;
+    });
+}
+
+int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!out && lanes && count) throw std::invalid_argument("null output");
+        if (rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
+        gpu_rng_probe(rng, stream0, lanes, count, sample, out);
+        return NRT_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+// Flattened scene as it lives in HBM (one copy per GPU, uploaded once).
+//
+// The reference's `Arc<dyn Hitable>` tree (scene_config.rs:277-381 ->
+// object.rs BVH + transforms) becomes:
+//   * one node array holding every threaded BVH (the top level and one per
+//     distinct instanced sub-scene, a "BLAS"), laid out depth-first so the
+//     left child of an inner node is the next node and each node carries a
+//     `skip` link to the first node after its subtree (END = -1 terminates
+//     the tree).  Depth-first, left-before-right order is exactly the
+//     reference's candidate order, so "the later candidate wins ties"
+//     reproduces `if hit_l.t < hit_r.t {l} else {r}` (object.rs:109-115).
+//   * primitives (sphere / quad / triangle) with the PlaneBuilder
+//     precomputation (plane.rs:381-413),
+//   * instances = a chain of Translate/Rotate/Scale applied outer -> inner to
+//     the ray, inner -> outer to the hit point/normal (translate.rs:37-49,
+//     rotate.rs:141-156, scale.rs:230-243), plus the BLAS root,
+//   * materials and textures (image texels as f32 RGB, row-major).
+// Layout is precision-templated: Real = double for the reference-exact
+// kernel, float for the fast kernel.  Nothing here is torch-aware.
+#pragma once
+
+#include <cstdint>
+
+namespace nrt {
+
+enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2 };
+enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2 };
+enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
+enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
+enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2 };
+
+constexpr int32_t NODE_END = -1;
+constexpr int MAX_INSTANCE_DEPTH = 4;
+
+template <typename Real>
+struct alignas(16) DNode {
+    Real bmin[3];   // AABB x/y/z .min (inner nodes only)
+    Real bmax[3];   // AABB x/y/z .max
+    uint32_t meta;  // kind | payload << 2 (payload = prim or instance index)
+    int32_t skip;   // next node after this subtree, or NODE_END
+};
+
+template <typename Real>
+struct alignas(16) DPrim {
+    Real a[3];  // sphere: center           plane: p
+    Real b[3];  // sphere: speed            plane: u
+    Real c[3];  //                          plane: v
+    Real n[3];  //                          plane: normal (unit)
+    Real w[3];  //                          plane: w = n / (n.n)
+    Real s;     // sphere: radius           plane: d = normal.p
+    uint32_t kind;
+    uint32_t material;
+};
+
+template <typename Real>
+struct alignas(16) DXform {
+    // TRANSLATE: m[0..2] = offset
+    // ROTATE:    m[0..8] = rotation (world->object), column major; inv[0..8] = inverse
+    // SCALE:     m = inverse scale matrix (world->object), inv = forward scale matrix,
+    //            both as 3x4 column major (cols 0..3, rows 0..2) of glam DMat4
+    Real m[12];
+    Real inv[12];
+    uint32_t kind;
+    uint32_t pad[3];
+};
+
+struct alignas(16) DInstance {
+    uint32_t first_xform;
+    uint32_t num_xforms;
+    int32_t root;  // BLAS root node (NODE_END = empty)
+    uint32_t pad;
+};
+
+struct alignas(16) DMaterial {
+    uint32_t kind;
+    uint32_t texture;
+    double param;  // Metal fuzz / Dielectric refraction index / DiffuseLight intensity
+};
+
+struct alignas(16) DTexture {
+    uint32_t kind;
+    uint32_t a, b;     // image: width, height; checker: even, odd texture ids
+    uint32_t pad;
+    uint64_t offset;   // image: first texel (float index / 3) in the texel array
+    double color[3];   // solid colour
+    double scale;      // checker scale
+};
+
+// What the kernel gets: device pointers + sizes (per precision).
+template <typename Real>
+struct DSceneView {
+    const DNode<Real>* nodes;
+    const DPrim<Real>* prims;
+    const DXform<Real>* xforms;
+    const DInstance* instances;
+    const DMaterial* materials;
+    const DTexture* textures;
+    const float* texels;
+    int32_t root;
+    int32_t max_depth;  // deepest instance nesting (0 = no instances)
+};
+
+}  // namespace nrt

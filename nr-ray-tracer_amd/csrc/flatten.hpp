@@ -1,0 +1,40 @@
+// Host-side flattening of the scene graph into the HBM layout of device_scene.hpp.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "device_scene.hpp"
+#include "scene.hpp"
+
+namespace nrt {
+
+struct FlatScene {
+    std::vector<DNode<double>> nodes;
+    std::vector<DPrim<double>> prims;
+    std::vector<DXform<double>> xforms;
+    std::vector<DInstance> instances;
+    std::vector<DMaterial> materials;
+    std::vector<DTexture> textures;
+    std::vector<float> texels;
+    int32_t root = NODE_END;
+    int32_t max_depth = 0;
+    uint32_t num_trees = 0;
+};
+
+FlatScene flatten_scene(const ObjectPtr& top_level_bvh);
+
+// Precision conversion for the fast kernel.  Boxes are rounded outward so an
+// f32 box always contains the f64 one.
+struct FlatScene32 {
+    std::vector<DNode<float>> nodes;
+    std::vector<DPrim<float>> prims;
+    std::vector<DXform<float>> xforms;
+};
+FlatScene32 to_f32(const FlatScene& s);
+
+// Canonical text form of the scene graph (used by the parity tests to compare
+// the C++ loader + BVH builder against the oracle's independent build).
+std::string dump_graph(const ObjectPtr& root);
+
+}  // namespace nrt

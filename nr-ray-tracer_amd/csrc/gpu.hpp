@@ -1,0 +1,24 @@
+// Host-side interface to the HIP layer (render.hip).  Plain C++ types only.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "render_params.hpp"
+
+namespace nrt {
+
+struct FlatScene;
+struct DeviceScene;
+
+int gpu_device_count();
+DeviceScene* gpu_upload_scene(const FlatScene& fs, int device);  // throws std::runtime_error
+void gpu_free_scene(DeviceScene* ds);
+size_t gpu_scene_bytes(const DeviceScene* ds);
+int gpu_scene_device(const DeviceScene* ds);
+// Enqueue one render launch on `stream` (nullptr = default stream). p.out is a device pointer.
+void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng, void* stream);
+// First `count` draws of `lanes` consecutive streams starting at stream0 (tests).
+void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out);
+
+}  // namespace nrt

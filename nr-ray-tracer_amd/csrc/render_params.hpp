@@ -1,0 +1,31 @@
+// Launch parameters of the path-tracing megakernel (host <-> device POD).
+#pragma once
+
+#include <cstdint>
+
+namespace nrt {
+
+enum : uint32_t { RNG_CHACHA8 = 0, RNG_PHILOX = 1 };
+
+struct RenderParams {
+    // Camera after CameraBuilder::build (camera.rs:205-227), always f64 on the host.
+    double top_left[3];
+    double pixel_delta_u[3];
+    double pixel_delta_v[3];
+    double look_from[3];
+    double defocus_disk_u[3];
+    double defocus_disk_v[3];
+    double background[3];
+    uint32_t width, height;
+    uint32_t spp;
+    uint32_t max_bounces;
+    // Rows rendered by this launch: y = row_offset + k * row_stride, k in [0, rows).
+    uint32_t row_offset, row_stride, rows;
+    // Pixel range inside the local (rows x width) buffer handled by this launch.
+    uint32_t pixel_begin, pixel_end;
+    float* out;  // rows * width * 3 floats, row-major (Rgb32FImage layout)
+    // Optional per-launch work counters (nullptr = off): see render.hip.
+    unsigned long long* counters;
+};
+
+}  // namespace nrt

@@ -1,0 +1,118 @@
+"""libnrt.so: loads, exports every symbol include/nrt.h declares, and its host
+logic behaves (no GPU compute here)."""
+import ctypes
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+import nrt
+from helpers import ROOT
+
+HEADER = os.path.join(ROOT, "include", "nrt.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nrt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol():
+    lib = ctypes.CDLL(nrt.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # the Python binding declares a signature for each of them
+    assert sorted(nrt.SIGNATURES) == syms
+
+
+def test_abi_version():
+    assert nrt.lib().nrt_abi_version() == 1
+
+
+def test_camera_builder_default_and_build():
+    b = nrt.CameraBuilder()
+    cam = b.build()
+    # CameraBuilder::default (camera.rs:162-203) then build (94-159)
+    assert (cam.width, cam.height, cam.samples_per_pixel, cam.ray_max_bounces) == (1200, 800, 10, 10)
+    h = math.tan(math.pi / 2 / 2.0)
+    vh = 1.0 * h * 2.0
+    vw = vh * (1200 / 800)
+    assert cam.pixel_delta_u[0] == pytest.approx(vw / 1200 / math.sqrt(2), rel=1e-12)
+    assert cam.look_from == (1.0, 1.0, 1.0)
+    b2 = nrt.CameraBuilder(samples_per_pixel=0).build()
+    assert b2.samples_per_pixel == 1  # samples_per_pixel.max(1)
+
+
+def test_camera_config_apply_degrees():
+    b = nrt.CameraBuilder().apply(nrt.CameraConfig(field_of_view=35.0, defocus_angle=0.5, width=10, height=20))
+    assert b.field_of_view == (35.0 * math.pi) / 180.0
+    assert b.defocus_angle == (0.5 * math.pi) / 180.0
+    assert (b.width, b.height) == (10, 20)
+
+
+def test_to_rgb8_matches_image_crate_rules():
+    x = np.array([0.0, 0.25, 1.0, 4.0, -1.0, np.nan, 0.5], dtype=np.float32)
+    got = nrt.to_rgb8(x, 0.5)
+    g = np.power(x, np.float32(0.5))
+    want = []
+    for v in g:
+        c = 1.0 if not (v < 1.0) else max(v, 0.0)
+        want.append(int(np.round(np.float32(c) * np.float32(255.0))))
+    assert got.tolist() == want
+
+
+def test_rows_selected():
+    s = nrt.Builder()
+    t = s.solid((0.5, 0.5, 0.5))
+    m = s.lambertian(t)
+    q = s.quad((0, 0, 0), (1, 0, 0), (0, 1, 0), m)
+    scene = s.finish(s.bvh([q]))
+    assert scene.rows_selected(1024, 0, 8) == 128
+    assert scene.rows_selected(10, 3, 4) == 2   # rows 3, 7
+    assert scene.rows_selected(10, 10, 4) == 0
+    assert scene.rows_selected(7, 0, 1) == 7
+
+
+def test_builder_errors_are_reported_not_fatal():
+    b = nrt.Builder()
+    with pytest.raises(nrt.NrtError) as ei:
+        b.lambertian(5)
+    assert ei.value.code == -1 and "texture handle" in str(ei.value)
+    t = b.solid((1, 1, 1))
+    m = b.lambertian(t)
+    sph = b.sphere((0, 0, 0), 1.0, m)
+    with pytest.raises(nrt.NrtError):
+        b.finish(sph)  # root must be a BVH
+
+
+def test_builder_matches_loader_dump():
+    # The constructor API builds the same graph as a scene file does.
+    b = nrt.Builder()
+    t = b.solid((0.5, 0.5, 0.5))
+    m = b.lambertian(t)
+    q = [b.quad((0, 0, 0), (1, 0, 0), (0, 1, 0), m), b.quad((0, 0, 1), (1, 0, 0), (0, 1, 0), m),
+         b.quad((0, 1, 0), (1, 0, 0), (0, 0, 1), m)]
+    inner = b.bvh(q)
+    obj = b.translate(b.rotate("y", b.scale(inner, (0.5, 2.0, 1.0)), 0.3), (1.0, 0.0, -1.0))
+    scene = b.finish(b.bvh([obj, b.sphere((0, 2, 0), 0.5, m)]))
+    d = scene.dump()
+    assert d.count("QUAD") == 3 and "SCALE" in d and "ROTATE" in d and "TRANSLATE" in d
+    st = scene.stats()
+    assert st["instances"] == 1 and st["xforms"] == 3 and st["prims"] == 4
+
+
+def test_render_without_gpu_fails_loudly():
+    if nrt.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    b = nrt.Builder()
+    m = b.lambertian(b.solid((1, 1, 1)))
+    scene = b.finish(b.bvh([b.sphere((0, 0, 0), 1.0, m)]))
+    cam = nrt.CameraBuilder(width=4, height=4, samples_per_pixel=1).build()
+    with pytest.raises(nrt.NrtError) as ei:
+        scene.render(cam)
+    assert ei.value.code == -3
