@@ -98,6 +98,18 @@ struct DSceneView {
     const float* texels;
     int32_t root;
     int32_t max_depth;  // deepest instance nesting (0 = no instances)
+    uint32_t n_nodes, n_prims, n_xforms, n_instances, n_materials, n_textures;
 };
+
+// Bytes of the LDS-stageable part of a scene (everything but texels), each
+// array starting on a 16-byte boundary, in the order nodes, prims, xforms,
+// instances, materials, textures.
+template <typename Real>
+inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
+    auto r16 = [](uint64_t b) { return (uint32_t)((b + 15) & ~uint64_t(15)); };
+    return r16(v.n_nodes * sizeof(DNode<Real>)) + r16(v.n_prims * sizeof(DPrim<Real>)) +
+           r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
+           r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture));
+}
 
 }  // namespace nrt

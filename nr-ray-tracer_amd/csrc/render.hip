@@ -1,615 +1,7 @@
-// MI355X (gfx950) megakernel for the reference's per-pixel path-tracing loop
-// (Camera::render, packages/ray-tracer-lib/src/camera.rs:302-343).
-//
-// One thread per pixel; each thread runs the pixel's samples in order over the
-// pixel's own RNG stream (camera.rs:318-329), an iterative bounce loop in
-// place of the recursive get_ray_color (camera.rs:269-300), and a stackless
-// traversal of the flattened, threaded BVH (device_scene.hpp) with t-narrowing.
-//
-// Template axes:
-//   Real  = double : the reference-exact variant (same operation order as
-//                    glam/rand, divisions kept, compiled with -ffp-contract=off)
-//   Real  = float  : the fast variant (reciprocal slab test, f32 RNG floats)
-//   RNG   = ChaCha8 per-pixel stream (rand_chacha 0.9, bit-exact with the
-//           reference) or Philox4x32-10 keyed per (pixel, sample, draw)
-//   MAXD  = 1 when instances do not nest (all BASELINE scenes), 4 otherwise.
-#include <hip/hip_runtime.h>
+// MI355X (gfx950) renderer: kernels live in kernel.hpp; this TU instantiates
+// them and holds the host side (device buffers, launches).  No torch types.
+#include "kernel.hpp"
 
-#include <cstdint>
-
-#include "device_scene.hpp"
-#include "render_params.hpp"
-
-namespace nrt {
-namespace dev {
-
-constexpr int BLOCK = 256;
-constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
-
-template <typename R>
-struct V {
-    R x, y, z;
-};
-template <typename R> __device__ __forceinline__ V<R> mk(R x, R y, R z) { return V<R>{x, y, z}; }
-template <typename R> __device__ __forceinline__ V<R> operator+(V<R> a, V<R> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-template <typename R> __device__ __forceinline__ V<R> operator-(V<R> a, V<R> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-template <typename R> __device__ __forceinline__ V<R> operator-(V<R> a) { return {-a.x, -a.y, -a.z}; }
-template <typename R> __device__ __forceinline__ V<R> operator*(R s, V<R> a) { return {s * a.x, s * a.y, s * a.z}; }
-template <typename R> __device__ __forceinline__ V<R> operator*(V<R> a, V<R> b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
-template <typename R> __device__ __forceinline__ V<R> operator/(V<R> a, R s) { return {a.x / s, a.y / s, a.z / s}; }
-template <typename R> __device__ __forceinline__ R dot(V<R> a, V<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-template <typename R> __device__ __forceinline__ V<R> cross(V<R> a, V<R> b) {
-    return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
-}
-template <typename R> __device__ __forceinline__ V<R> normalize(V<R> a) {
-    return (R(1) / sqrt(dot(a, a))) * a;  // glam: self * self.length().recip()
-}
-template <typename R> __device__ __forceinline__ V<R> ld3(const R* p) { return {p[0], p[1], p[2]}; }
-template <typename R> __device__ __forceinline__ V<R> ld3d(const double* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
-
-// glam DMat3 * v = (c0*x + c1*y) + c2*z, column major m[3c+r]
-template <typename R> __device__ __forceinline__ V<R> mat3(const R* m, V<R> v) {
-    V<R> c0 = ld3(m), c1 = ld3(m + 3), c2 = ld3(m + 6);
-    return (v.x * c0 + v.y * c1) + v.z * c2;
-}
-// glam DMat4::transform_point3 / transform_vector3 on a 3x4 column-major block
-template <typename R> __device__ __forceinline__ V<R> xf_point(const R* m, V<R> v) {
-    V<R> r;
-    R* o = &r.x;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        R res = m[k] * v.x;
-        res = m[3 + k] * v.y + res;
-        res = m[6 + k] * v.z + res;
-        res = m[9 + k] + res;
-        o[k] = res;
-    }
-    return r;
-}
-template <typename R> __device__ __forceinline__ V<R> xf_vector(const R* m, V<R> v) {
-    V<R> r;
-    R* o = &r.x;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        R res = m[k] * v.x;
-        res = m[3 + k] * v.y + res;
-        res = m[6 + k] * v.z + res;
-        o[k] = res;
-    }
-    return r;
-}
-
-// f64::signum: 1 for +0/positive, -1 for -0/negative, NaN for NaN
-template <typename R> __device__ __forceinline__ R signum(R x) { return x != x ? x : copysign(R(1), x); }
-
-// ----------------------------------------------------------------------- RNG
-// rand_chacha 0.9 ChaCha8Rng::seed_from_u64(0): key = PCG32 expansion of 0.
-__constant__ const uint32_t CHACHA_KEY[8] = {0xf973f2ecu, 0x45cdb581u, 0x7346f087u, 0xad6cad06u,
-                                              0xe3a3d0d0u, 0x67e71733u, 0x72ea9bf2u, 0xfe7d8ad7u};
-
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
-
-#define NRT_QR(a, b, c, d)              \
-    a += b; d ^= a; d = rotl32(d, 16);  \
-    c += d; b ^= c; b = rotl32(b, 12);  \
-    a += b; d ^= a; d = rotl32(d, 8);   \
-    c += d; b ^= c; b = rotl32(b, 7);
-
-// One ChaCha8 block (state words 12-13 = 64-bit block counter, 14-15 = stream).
-__device__ __forceinline__ void chacha8_block(uint32_t ctr_lo, uint32_t ctr_hi, uint32_t s_lo, uint32_t s_hi,
-                                              uint32_t out[16]) {
-    const uint32_t i0 = 0x61707865u, i1 = 0x3320646eu, i2 = 0x79622d32u, i3 = 0x6b206574u;
-    uint32_t x0 = i0, x1 = i1, x2 = i2, x3 = i3;
-    uint32_t x4 = CHACHA_KEY[0], x5 = CHACHA_KEY[1], x6 = CHACHA_KEY[2], x7 = CHACHA_KEY[3];
-    uint32_t x8 = CHACHA_KEY[4], x9 = CHACHA_KEY[5], x10 = CHACHA_KEY[6], x11 = CHACHA_KEY[7];
-    uint32_t x12 = ctr_lo, x13 = ctr_hi, x14 = s_lo, x15 = s_hi;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        NRT_QR(x0, x4, x8, x12) NRT_QR(x1, x5, x9, x13) NRT_QR(x2, x6, x10, x14) NRT_QR(x3, x7, x11, x15)
-        NRT_QR(x0, x5, x10, x15) NRT_QR(x1, x6, x11, x12) NRT_QR(x2, x7, x8, x13) NRT_QR(x3, x4, x9, x14)
-    }
-    out[0] = x0 + i0; out[1] = x1 + i1; out[2] = x2 + i2; out[3] = x3 + i3;
-    out[4] = x4 + CHACHA_KEY[0]; out[5] = x5 + CHACHA_KEY[1]; out[6] = x6 + CHACHA_KEY[2]; out[7] = x7 + CHACHA_KEY[3];
-    out[8] = x8 + CHACHA_KEY[4]; out[9] = x9 + CHACHA_KEY[5]; out[10] = x10 + CHACHA_KEY[6]; out[11] = x11 + CHACHA_KEY[7];
-    out[12] = x12 + ctr_lo; out[13] = x13 + ctr_hi; out[14] = x14 + s_lo; out[15] = x15 + s_hi;
-}
-
-// Per-pixel ChaCha8 stream = ChaCha8Rng::seed_from_u64(0) + set_stream(n)
-// (camera.rs:318-320); every draw is a next_u64 (two consecutive keystream
-// words).  Keystream words wait in an LDS ring of 16 u64 slots per lane.
-// Refills are batched per wave: when any active lane is empty, every active
-// lane with room for a block generates one, so a wave computes about one
-// block per 8-9 draw steps even when lanes have drifted apart.
-struct ChaCha8 {
-    static constexpr bool uses_lds = true;
-    uint32_t s_lo, s_hi, ctr, head, count;
-    uint2* ring;  // slot k of this lane at ring[k * BLOCK]
-
-    __device__ __forceinline__ void init(uint64_t stream, uint2* base) {
-        s_lo = (uint32_t)stream;
-        s_hi = (uint32_t)(stream >> 32);
-        ctr = 0;
-        head = 0;
-        count = 0;
-        ring = base;
-    }
-    __device__ __forceinline__ void start_sample(uint32_t) {}
-    __device__ __forceinline__ void refill() {
-        uint32_t w[16];
-        chacha8_block(ctr, 0u, s_lo, s_hi, w);
-        ++ctr;
-        uint32_t slot = (head + count) & (RING - 1);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            ring[slot * BLOCK] = make_uint2(w[2 * k], w[2 * k + 1]);
-            slot = (slot + 1) & (RING - 1);
-        }
-        count += 8;
-    }
-    __device__ __forceinline__ uint64_t next() {
-        if (__ballot(count == 0) != 0ull) {
-            if (count <= RING - 8) refill();
-        }
-        const uint2 v = ring[head * BLOCK];
-        head = (head + 1) & (RING - 1);
-        --count;
-        return (uint64_t)v.x | ((uint64_t)v.y << 32);
-    }
-};
-
-// Philox4x32-10 (Salmon et al. 2011), counter = (pixel, sample, pair, 0), key = (0, 0).
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1, uint32_t out[4]) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-    }
-    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
-}
-
-struct Philox {
-    static constexpr bool uses_lds = false;
-    uint32_t pix, sample, pair;
-    uint64_t spare;
-    bool has_spare;
-    __device__ __forceinline__ void init(uint64_t stream, uint2*) {
-        pix = (uint32_t)stream;
-        sample = 0;
-        pair = 0;
-        has_spare = false;
-    }
-    __device__ __forceinline__ void start_sample(uint32_t s) {
-        sample = s;
-        pair = 0;
-        has_spare = false;
-    }
-    __device__ __forceinline__ uint64_t next() {
-        if (has_spare) {
-            has_spare = false;
-            return spare;
-        }
-        uint32_t w[4];
-        philox4x32_10(pix, sample, pair, 0u, 0u, 0u, w);
-        ++pair;
-        spare = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-        has_spare = true;
-        return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-    }
-};
-
-// rand 0.9 `random_range(low..high)` / `(low..=high)` on f64: one draw,
-// value1_2 = from_bits((u >> 12) | 1.0.to_bits()), (value1_2 - 1) * scale + low.
-template <typename R> struct Uniform;
-template <> struct Uniform<double> {
-    static __device__ __forceinline__ double range(uint64_t u, double low, double high) {
-        const double v12 = __longlong_as_double((long long)((u >> 12) | 0x3FF0000000000000ull));
-        const double scale = high - low;
-        return (v12 - 1.0) * scale + low;
-    }
-};
-template <> struct Uniform<float> {
-    static __device__ __forceinline__ float range(uint64_t u, float low, float high) {
-        const float v12 = __uint_as_float(0x3F800000u | (uint32_t)(u >> 41));
-        return (v12 - 1.0f) * (high - low) + low;
-    }
-};
-
-// vector.rs:61-70 — rejection in [-1,1)^3 until 1e-160 < |p|^2 <= 1, returns p/|p|^2
-template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sphere(G& g) {
-    while (true) {
-        const R x = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R y = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R z = Uniform<R>::range(g.next(), R(-1), R(1));
-        const V<R> p = mk(x, y, z);
-        const R ls = dot(p, p);
-        const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
-        if (tiny < ls && ls <= R(1)) return p / ls;
-    }
-}
-// vector.rs:72-81 — rejection in [-1,1)^2 until |p|^2 < 1, returns p/|p|^2
-template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_disk(G& g) {
-    while (true) {
-        const R x = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R y = Uniform<R>::range(g.next(), R(-1), R(1));
-        const V<R> p = mk(x, y, R(0));
-        const R ls = dot(p, p);
-        if (ls < R(1)) return p / ls;
-    }
-}
-
-// ----------------------------------------------------------------- geometry
-template <typename R>
-struct Ray {
-    V<R> o, d;
-    V<R> inv;  // 1/d (fast variant only)
-    R time;
-};
-
-template <typename R, bool EXACT> __device__ __forceinline__ void prep_ray(Ray<R>& r) {
-    if constexpr (!EXACT) r.inv = mk(R(1) / r.d.x, R(1) / r.d.y, R(1) / r.d.z);
-}
-
-// AABB::hit (aabb.rs:110-132) with range (0.001, t_max); t_max narrows during traversal.
-template <typename R, bool EXACT>
-__device__ __forceinline__ bool box_hit(const DNode<R>& n, const Ray<R>& r, R t_max) {
-    R lo = R(0.001), hi = t_max;
-    const R* o = &r.o.x;
-    const R* d = &r.d.x;
-    const R* iv = &r.inv.x;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        R a, b;
-        if constexpr (EXACT) {
-            a = (n.bmin[k] - o[k]) / d[k];
-            b = (n.bmax[k] - o[k]) / d[k];
-        } else {
-            a = (n.bmin[k] - o[k]) * iv[k];
-            b = (n.bmax[k] - o[k]) * iv[k];
-        }
-        const bool lt = a < b;  // Interval::ensure
-        const R elo = lt ? a : b, ehi = lt ? b : a;
-        lo = fmax(lo, elo);
-        hi = fmin(hi, ehi);
-    }
-    return !(lo > hi);
-}
-
-template <typename R>
-struct Hit {
-    R t;
-    V<R> p, n;
-    R u, v;
-    bool front;
-    uint32_t mat;
-};
-
-// HitRecord::new_with_uv (hitable.rs:38-59)
-template <typename R>
-__device__ __forceinline__ void face(Hit<R>& h, V<R> dir, V<R> outward) {
-    const R sign = signum(dot(dir, outward));
-    h.front = sign < R(0);
-    h.n = (-sign) * outward;
-}
-
-// Sphere::hit (sphere.rs:105-163) with range (0.001, inf); returns t or -1.
-template <typename R>
-__device__ __forceinline__ R sphere_t(const DPrim<R>& s, const Ray<R>& r, V<R>& center) {
-    center = ld3(s.a) + r.time * ld3(s.b);
-    const V<R> ec = center - r.o;
-    const R a = dot(r.d, r.d);
-    const R h = dot(ec, r.d);
-    const R c = dot(ec, ec) - s.s * s.s;
-    const R disc = h * h - a * c;
-    if (disc < R(0)) return R(-1);
-    const R sq = sqrt(disc);
-    R t = (h - sq) / a;
-    if (R(0.001) < t && t < R(INFINITY)) return t;
-    t = (h + sq) / a;
-    if (R(0.001) < t && t < R(INFINITY)) return t;
-    return R(-1);
-}
-
-template <typename R>
-__device__ __forceinline__ void sphere_record(Hit<R>& h, const Ray<R>& r, R t, V<R> center) {
-    h.p = r.o + t * r.d;
-    const V<R> nrm = normalize(h.p - center);
-    const R theta = acos(-nrm.y);
-    const R phi = atan2(-nrm.z, nrm.x) + R(M_PI);
-    h.u = phi / (R(2.0) * R(M_PI));
-    h.v = theta / R(M_PI);
-    face(h, r.d, nrm);
-}
-
-// Plane::hit (plane.rs:141-174) with range [0.001, inf]; returns t or -1.
-template <typename R>
-__device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alpha, R& beta, V<R>& point) {
-    const V<R> nrm = ld3(q.n);
-    const R denom = dot(nrm, r.d);
-    if (fabs(denom) < R(1e-8)) return R(-1);
-    const R t = (q.s - dot(nrm, r.o)) / denom;
-    if (!(R(0.001) <= t && t <= R(INFINITY))) return R(-1);
-    point = r.o + t * r.d;
-    const V<R> ph = point - ld3(q.a);
-    alpha = dot(ld3(q.w), cross(ph, ld3(q.c)));
-    beta = dot(ld3(q.w), cross(ld3(q.b), ph));
-    bool inside;
-    if (q.kind == PRIM_QUAD)
-        inside = (R(0) <= alpha && alpha <= R(1)) && (R(0) <= beta && beta <= R(1));
-    else
-        inside = alpha > R(0) && beta > R(0) && (alpha + beta) < R(1);
-    return inside ? t : R(-1);
-}
-
-// ray into object space through an instance's chain (outer -> inner)
-template <typename R, bool EXACT>
-__device__ __forceinline__ void xform_in(const DSceneView<R>& sc, const DInstance& inst, Ray<R>& r) {
-    for (uint32_t k = 0; k < inst.num_xforms; ++k) {
-        const DXform<R>& x = sc.xforms[inst.first_xform + k];
-        if (x.kind == XF_TRANSLATE) {
-            r.o = r.o - ld3(x.m);
-        } else if (x.kind == XF_ROTATE) {
-            r.o = mat3(x.m, r.o);
-            r.d = mat3(x.m, r.d);
-        } else {
-            r.o = xf_point(x.m, r.o);
-            r.d = xf_vector(x.m, r.d);
-        }
-    }
-    prep_ray<R, EXACT>(r);
-}
-
-// hit point / normal back out (inner -> outer); Scale leaves the normal alone (scale.rs:239-242)
-template <typename R>
-__device__ __forceinline__ void xform_out(const DSceneView<R>& sc, const DInstance& inst, Hit<R>& h) {
-    for (uint32_t k = inst.num_xforms; k-- > 0;) {
-        const DXform<R>& x = sc.xforms[inst.first_xform + k];
-        if (x.kind == XF_TRANSLATE) {
-            h.p = h.p + ld3(x.m);
-        } else if (x.kind == XF_ROTATE) {
-            h.p = mat3(x.inv, h.p);
-            h.n = mat3(x.inv, h.n);
-        } else {
-            h.p = xf_point(x.inv, h.p);
-        }
-    }
-}
-
-// Closest hit over the flattened scene.  Candidates arrive in the reference's
-// depth-first, left-before-right order, so `t <= t_best` (the later candidate
-// wins a tie) reproduces BVH::hit's `if l.t < r.t {l} else {r}`.
-template <typename R, int MAXD, bool EXACT>
-__device__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, Hit<R>& hit) {
-    R t_best = R(INFINITY);
-    bool found = false;
-    int32_t node = sc.root;
-    int depth = 0;
-    int32_t ret[MAXD];
-    uint32_t inst_id[MAXD];
-    Ray<R> saved[MAXD];
-    Ray<R> ray = wray;
-    while (true) {
-        if (node < 0) {
-            if (depth == 0) break;
-            --depth;
-            node = ret[depth];
-            if constexpr (MAXD == 1) ray = wray;
-            else ray = depth == 0 ? wray : saved[depth];
-            continue;
-        }
-        const DNode<R>& nd = sc.nodes[node];
-        const uint32_t meta = nd.meta;
-        const uint32_t kind = meta & 3u;
-        if (kind == NODE_INNER) {
-            node = box_hit<R, EXACT>(nd, ray, t_best) ? node + 1 : nd.skip;
-        } else if (kind == NODE_PRIM) {
-            const DPrim<R>& pr = sc.prims[meta >> 2];
-            Hit<R> cand;
-            bool ok = false;
-            if (pr.kind == PRIM_SPHERE) {
-                V<R> center;
-                const R t = sphere_t(pr, ray, center);
-                if (t >= R(0) && t <= t_best) {
-                    cand.t = t;
-                    sphere_record(cand, ray, t, center);
-                    ok = true;
-                }
-            } else {
-                R alpha, beta;
-                V<R> point;
-                const R t = plane_t(pr, ray, alpha, beta, point);
-                if (t >= R(0) && t <= t_best) {
-                    cand.t = t;
-                    cand.p = point;
-                    cand.u = alpha;
-                    cand.v = beta;
-                    face(cand, ray.d, ld3(pr.n));
-                    ok = true;
-                }
-            }
-            if (ok) {
-                cand.mat = pr.material;
-                for (int l = depth - 1; l >= 0; --l) xform_out(sc, sc.instances[inst_id[l]], cand);
-                t_best = cand.t;
-                hit = cand;
-                found = true;
-            }
-            node = nd.skip;
-        } else {
-            const DInstance inst = sc.instances[meta >> 2];
-            ret[depth] = nd.skip;
-            inst_id[depth] = meta >> 2;
-            if constexpr (MAXD > 1) saved[depth] = ray;
-            ++depth;
-            xform_in<R, EXACT>(sc, inst, ray);
-            node = inst.root;
-        }
-    }
-    return found;
-}
-
-// ----------------------------------------------------------------- shading
-// Texture::get_color (solid_color.rs:45-53, image.rs:83-94, checker.rs:170-184)
-template <typename R>
-__device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v) {
-    for (int guard = 0; guard < 64; ++guard) {
-        const DTexture& t = sc.textures[tid];
-        if (t.kind == TEX_SOLID) return ld3d<R>(t.color);
-        if (t.kind == TEX_IMAGE) {
-            const R cu = u < R(0) ? R(0) : (u > R(1) ? R(1) : u);  // f64::clamp keeps NaN
-            const R cv = v < R(0) ? R(0) : (v > R(1) ? R(1) : v);
-            const R fx = cu * (R)t.a;
-            const R fy = (R(1) - cv) * (R)t.b;
-            // `as u32` saturates (NaN -> 0); index W/H would panic in the
-            // reference (Q12): clamped to the last texel here.
-            uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
-            uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)t.b ? t.b - 1 : (uint32_t)fy);
-            const float* px = sc.texels + 3ull * (t.offset + (uint64_t)y * t.a + x);
-            return mk((R)px[0], (R)px[1], (R)px[2]);
-        }
-        // Checker: (uv * scale).as_u64vec2() summed, parity selects even/odd
-        const R su = u * (R)t.scale, sv = v * (R)t.scale;
-        const uint64_t iu = !(su > R(0)) ? 0ull : (su >= R(18446744073709551615.0) ? ~0ull : (uint64_t)su);
-        const uint64_t iv = !(sv > R(0)) ? 0ull : (sv >= R(18446744073709551615.0) ? ~0ull : (uint64_t)sv);
-        tid = ((iu + iv) % 2 == 0) ? t.a : t.b;
-    }
-    return mk(R(0), R(0), R(0));
-}
-
-template <typename R> __device__ __forceinline__ V<R> reflect(V<R> v, V<R> n) {
-    return v - ((R(2.0) * dot(v, n)) * n);
-}
-template <typename R> __device__ __forceinline__ V<R> refract(V<R> i, V<R> n, R eta) {
-    const R ndi = dot(n, i);
-    const R k = R(1.0) - eta * eta * (R(1.0) - ndi * ndi);
-    if (k >= R(0)) return (eta * i) - ((eta * ndi + sqrt(k)) * n);
-    return mk(R(0), R(0), R(0));
-}
-// dielectric.rs:13-19 (powi(5) = x * ((x*x)*(x*x)))
-template <typename R> __device__ __forceinline__ R reflectance(R cosine, R ri) {
-    R r0 = (R(1.0) - ri) / (R(1.0) + ri);
-    r0 = r0 * r0;
-    const R x = R(1.0) - cosine;
-    const R x2 = x * x;
-    return r0 + (R(1.0) - r0) * (x * (x2 * x2));
-}
-
-template <typename R> struct Accum;
-template <> struct Accum<double> { using T = double; };
-template <> struct Accum<float> { using T = double; };
-
-// ------------------------------------------------------------------ kernel
-template <typename R, class G, int MAXD, bool EXACT>
-__global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, const DSceneView<R> sc) {
-    __shared__ uint2 ring_lds[G::uses_lds ? RING * BLOCK : 1];
-    const uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= p.pixel_end) return;
-    const uint32_t x = i % p.width;
-    const uint32_t row = i / p.width;
-    const uint32_t y = p.row_offset + row * p.row_stride;
-    const uint64_t n = (uint64_t)y * p.width + x;  // pixel index = RNG stream (camera.rs:320-323)
-
-    G g;
-    g.init(n, &ring_lds[G::uses_lds ? threadIdx.x : 0]);
-
-    const V<R> top_left = ld3d<R>(p.top_left), du = ld3d<R>(p.pixel_delta_u), dv = ld3d<R>(p.pixel_delta_v);
-    const V<R> look_from = ld3d<R>(p.look_from), disk_u = ld3d<R>(p.defocus_disk_u),
-               disk_v = ld3d<R>(p.defocus_disk_v);
-    const V<R> background = ld3d<R>(p.background);
-
-    double sx = 0.0, sy = 0.0, sz = 0.0;
-    for (uint32_t s = 0; s < p.spp; ++s) {
-        g.start_sample(s);
-        // Camera::get_ray (camera.rs:244-267)
-        R ox = R(0), oy = R(0);
-        if (p.spp > 1) {
-            ox = Uniform<R>::range(g.next(), R(-0.5), R(0.5));
-            oy = Uniform<R>::range(g.next(), R(-0.5), R(0.5));
-        }
-        const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
-        const V<R> disk = random_in_unit_disk<R>(g);
-        Ray<R> ray;
-        ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
-        ray.d = point - ray.o;
-        ray.time = Uniform<R>::range(g.next(), R(0.0), R(1.0));
-        prep_ray<R, EXACT>(ray);
-        bool bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
-
-        // get_ray_color (camera.rs:269-300), iteratively: L = a0*(a1*(...*T))
-        V<R> tp = mk(R(1), R(1), R(1));
-        V<R> result = mk(R(0), R(0), R(0));
-        for (uint32_t b = 0;; ++b) {
-            if (b >= p.max_bounces) break;  // depth cap returns black (Q6)
-            Hit<R> h;
-            if (!trace<R, MAXD, EXACT>(sc, ray, h)) {
-                result = tp * background;
-                break;
-            }
-            const DMaterial m = sc.materials[h.mat];
-            if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
-                const R k = bounced ? (R)m.param : R(1.0);
-                result = tp * (k * tex_color(sc, m.texture, h.u, h.v));
-                break;
-            }
-            V<R> dir;
-            V<R> att = mk(R(1), R(1), R(1));
-            if (m.kind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
-                const R ri = h.front ? R(1.0) / (R)m.param : (R)m.param;
-                const V<R> unit = normalize(ray.d);
-                const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
-                const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
-                bool refl = ri * sin_theta > R(1.0);
-                if (!refl) refl = reflectance(cos_theta, ri) > Uniform<R>::range(g.next(), R(0.0), R(1.0));
-                dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
-            } else {
-                const V<R> rs = random_in_unit_sphere<R>(g);
-                if (m.kind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
-                    dir = h.n + rs;
-                    if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
-                } else {  // metal.rs:73-91 (draws even when fuzz = 0, Q5)
-                    dir = normalize(reflect(ray.d, h.n)) + (R)m.param * rs;
-                    if (!(dot(dir, h.n) > R(0.0))) break;  // absorbed: emitted = 0
-                }
-                att = tex_color(sc, m.texture, h.u, h.v);
-            }
-            tp = tp * att;
-            ray.o = h.p;
-            ray.d = dir;
-            prep_ray<R, EXACT>(ray);
-            bounced = true;
-        }
-        sx += (double)result.x;
-        sy += (double)result.y;
-        sz += (double)result.z;
-    }
-    const double inv = (double)p.spp;
-    float* o = p.out + 3ull * i;
-    o[0] = (float)(sx / inv);
-    o[1] = (float)(sy / inv);
-    o[2] = (float)(sz / inv);
-}
-
-// First `count` next_u64 draws of a ChaCha8 / Philox stream (tests only).
-template <class G>
-__global__ void __launch_bounds__(BLOCK) rng_probe_kernel(uint64_t stream0, uint32_t count, uint32_t sample,
-                                                          unsigned long long* out) {
-    __shared__ uint2 ring_lds[G::uses_lds ? RING * BLOCK : 1];
-    const uint64_t stream = stream0 + threadIdx.x;
-    G g;
-    g.init(stream, &ring_lds[G::uses_lds ? threadIdx.x : 0]);
-    g.start_sample(sample);
-    for (uint32_t k = 0; k < count; ++k) out[(uint64_t)threadIdx.x * count + k] = g.next();
-}
-
-}  // namespace dev
-}  // namespace nrt
-
-// =====================================================================
-// Host side: device buffers and launches (no torch types, plain HIP).
-// =====================================================================
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -618,6 +10,9 @@ __global__ void __launch_bounds__(BLOCK) rng_probe_kernel(uint64_t stream0, uint
 #include "flatten.hpp"
 #include "gpu.hpp"
 
+// =====================================================================
+// Host side: device buffers and launches (no torch types, plain HIP).
+// =====================================================================
 namespace nrt {
 
 namespace {
@@ -668,8 +63,11 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* mats = (DMaterial*)track(upload(fs.materials, "materials"), fs.materials.size() * sizeof(DMaterial));
         auto* texs = (DTexture*)track(upload(fs.textures, "textures"), fs.textures.size() * sizeof(DTexture));
         auto* texels = (float*)track(upload(fs.texels, "texels"), fs.texels.size() * sizeof(float));
-        ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth};
-        ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root, fs.max_depth};
+        const uint32_t nn = (uint32_t)fs.nodes.size(), np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
+                       ni = (uint32_t)fs.instances.size(), nm = (uint32_t)fs.materials.size(),
+                       nt = (uint32_t)fs.textures.size();
+        ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth, nn, np, nx, ni, nm, nt};
+        ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root, fs.max_depth, nn, np, nx, ni, nm, nt};
     } catch (...) {
         gpu_free_scene(ds);
         throw;
@@ -690,11 +88,22 @@ void gpu_free_scene(DeviceScene* ds) {
 size_t gpu_scene_bytes(const DeviceScene* ds) { return ds ? ds->bytes : 0; }
 int gpu_scene_device(const DeviceScene* ds) { return ds ? ds->device : -1; }
 
+// Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
+constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
+
 template <typename R, class G, int MAXD, bool EXACT>
 static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_t stream) {
     const uint32_t n = p.pixel_end - p.pixel_begin;
     const uint32_t blocks = (n + dev::BLOCK - 1) / dev::BLOCK;
-    hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT>), dim3(blocks), dim3(dev::BLOCK), 0, stream, p, v);
+    const uint32_t ring = G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0;
+    const uint32_t scene = lds_scene_bytes(v);
+    if (scene <= LDS_SCENE_LIMIT) {
+        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true>), dim3(blocks), dim3(dev::BLOCK), ring + scene,
+                           stream, p, v);
+    } else {
+        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, false>), dim3(blocks), dim3(dev::BLOCK), ring,
+                           stream, p, v);
+    }
 }
 
 void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng,
@@ -729,7 +138,8 @@ void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t coun
     const size_t bytes = (size_t)lanes * count * sizeof(unsigned long long);
     check(hipMalloc((void**)&d, bytes ? bytes : 8), "hipMalloc(rng probe)");
     if (rng == RNG_CHACHA8)
-        hipLaunchKernelGGL(dev::rng_probe_kernel<dev::ChaCha8>, dim3(1), dim3(lanes), 0, 0, stream0, count, sample, d);
+        hipLaunchKernelGGL(dev::rng_probe_kernel<dev::ChaCha8>, dim3(1), dim3(lanes),
+                           dev::RING * dev::BLOCK * sizeof(uint2), 0, stream0, count, sample, d);
     else
         hipLaunchKernelGGL(dev::rng_probe_kernel<dev::Philox>, dim3(1), dim3(lanes), 0, 0, stream0, count, sample, d);
     hipError_t e = hipGetLastError();

@@ -122,6 +122,14 @@ def lib() -> C.CDLL:
     """Load libnrt.so (built in-tree by __graft_entry__.build()); raise if absent."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch wheels bundle their own
+        # libamdhip64.so (same soname).  Loading torch first makes libnrt bind to
+        # that copy instead of pulling /opt/rocm's beside it.
+        if os.environ.get("NRT_NO_TORCH") != "1":
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not os.path.exists(LIB_PATH):
             raise NrtError(-3, f"{LIB_PATH} not built: run __graft_entry__.build() / make -C nr-ray-tracer_amd")
         L = C.CDLL(LIB_PATH)

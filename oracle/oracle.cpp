@@ -981,21 +981,23 @@ int main(int argc, char** argv) {
         const std::string out = argv[3];
         unsigned threads = std::thread::hardware_concurrency();
         uint32_t row_off = 0, row_stride = 1;
-        std::string stats;
+        std::string stats, var_path;
         for (int i = 4; i < argc; ++i) {
             const std::string a = argv[i];
             if (a == "--threads" && i + 1 < argc) threads = (unsigned)atoi(argv[++i]);
             else if (a == "--rows" && i + 2 < argc) { row_off = (uint32_t)atoi(argv[++i]); row_stride = (uint32_t)atoi(argv[++i]); }
             else if (a == "--spp" && i + 1 < argc) sc.camera.samples_per_pixel = U(argv[++i]);
             else if (a == "--stats" && i + 1 < argc) stats = argv[++i];
+            else if (a == "--var" && i + 1 < argc) var_path = argv[++i];
         }
+        const bool want_var = !var_path.empty();
         if (threads < 1) threads = 1;
         const Camera& cam = sc.camera;
         const uint32_t W = (uint32_t)cam.width, H = (uint32_t)cam.height;
         std::vector<uint32_t> rows;
         for (uint32_t y = row_off; y < H; y += row_stride) rows.push_back(y);
         const size_t npix = rows.size() * W;
-        std::vector<float> img(npix * 3);
+        std::vector<float> img(npix * 3), var(want_var ? npix * 3 : 0);
         std::atomic<size_t> next{0};
         std::vector<Counters> all(threads);
         const auto t0 = std::chrono::steady_clock::now();
@@ -1010,10 +1012,19 @@ int main(int argc, char** argv) {
                     const uint32_t n = y * W + x;
                     ChaCha8Rng rng = ChaCha8Rng::seed_from_u64(0);
                     rng.set_stream(n);
-                    DVec3 s{0, 0, 0};
+                    DVec3 s{0, 0, 0}, sq{0, 0, 0};
                     for (uint64_t k2 = 0; k2 < cam.samples_per_pixel; ++k2) {
                         const Ray ray = cam.get_ray(x, y, rng);
-                        s = s + cam.get_ray_color(ray, 0, *sc.root, rng);
+                        const DVec3 c = cam.get_ray_color(ray, 0, *sc.root, rng);
+                        s = s + c;
+                        if (want_var) sq = sq + c * c;
+                    }
+                    if (want_var) {  // unbiased per-sample variance (test statistics only)
+                        const double m = (double)cam.samples_per_pixel;
+                        const double dd = m > 1 ? m - 1 : 1;
+                        var[3 * i + 0] = (float)((sq.x - s.x * s.x / m) / dd);
+                        var[3 * i + 1] = (float)((sq.y - s.y * s.y / m) / dd);
+                        var[3 * i + 2] = (float)((sq.z - s.z * s.z / m) / dd);
                     }
                     NRT_COUNT(tl.draws += rng.draws);
                     const DVec3 c = s / (double)cam.samples_per_pixel;
@@ -1030,6 +1041,12 @@ int main(int argc, char** argv) {
         if (!f) { fprintf(stderr, "cannot write %s\n", out.c_str()); return 2; }
         fwrite(img.data(), sizeof(float), img.size(), f);
         fclose(f);
+        if (want_var) {
+            FILE* vf = fopen(var_path.c_str(), "wb");
+            if (!vf) { fprintf(stderr, "cannot write %s\n", var_path.c_str()); return 2; }
+            fwrite(var.data(), sizeof(float), var.size(), vf);
+            fclose(vf);
+        }
         Counters tot;
         for (auto& c : all) {
             tot.aabb_tests += c.aabb_tests; tot.sphere_tests += c.sphere_tests; tot.sphere_hits += c.sphere_hits;

@@ -43,13 +43,17 @@ def oracle_tree(scene, workdir, width=None, height=None, spp=None, bounces=None)
     return path, cam
 
 
-def oracle_render(tree, threads=None, rows=(0, 1), stats=False, spp=None):
+def oracle_render(tree, threads=None, rows=(0, 1), stats=False, spp=None, var=False):
+    """Run the oracle; returns (image, info) or (image, info, per-sample variance) with var=True."""
     ensure_oracle()
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "img.f32")
         st = os.path.join(td, "stats.json")
+        vp = os.path.join(td, "var.f32")
         cmd = [ORACLE_STATS_BIN if stats else ORACLE_BIN, "render", tree, out, "--rows", str(rows[0]), str(rows[1]),
                "--stats", st]
+        if var:
+            cmd += ["--var", vp]
         if threads:
             cmd += ["--threads", str(threads)]
         if spp:
@@ -59,6 +63,8 @@ def oracle_render(tree, threads=None, rows=(0, 1), stats=False, spp=None):
         img = np.fromfile(out, dtype="<f4")
         with open(st) as fh:
             info = json.load(fh)
+        if var:
+            return img, info, np.fromfile(vp, dtype="<f4")
         return img, info
 
 

@@ -91,23 +91,53 @@ def test_row_interleave_is_bitwise_identical():
     np.testing.assert_array_equal(want, s.render(precision="f64", rng="chacha8", row_offset=1, row_stride=3))
 
 
+STAT_CASES = [("scenes/cornell-box-scene.json", 48, 48, 64), ("scenes/spheres.toml", 64, 36, 32),
+              ("scenes/cube-scene.json", 40, 30, 32)]
+
+
 @pytest.mark.parametrize("precision,rng", [("f32", "chacha8"), ("f32", "philox"), ("f64", "philox")])
-def test_fast_variants_statistically_match(precision, rng):
-    scene, w, h, spp = "scenes/cornell-box-scene.json", 48, 48, 64
-    want = reference(scene, w, h, spp).reshape(h, w, 3).astype(np.float64)
+@pytest.mark.parametrize("case", STAT_CASES, ids=[c[0] for c in STAT_CASES])
+def test_fast_variants_statistically_match(precision, rng, case):
+    """Statistical parity: image means within 4.5 standard errors,
+    per-pixel z-scores (std from the oracle's per-sample variance) with mean
+    z^2 in [0.5, 2] and < 1 % of pixels beyond |z| > 6."""
+    scene, w, h, spp = case
+    with tempfile.TemporaryDirectory() as td:
+        tree, _ = oracle_tree(scene, td, width=w, height=h, spp=spp)
+        want, _, var = oracle_render(tree, var=True)
+    want = want.astype(np.float64)
+    var = np.maximum(var.astype(np.float64), 0.0)
     s = load(scene, w, h, spp)
-    got = s.render(precision=precision, rng=rng).astype(np.float64)
+    got = s.render(precision=precision, rng=rng).reshape(-1).astype(np.float64)
     assert np.all(np.isfinite(got))
-    m_got, m_want = got.mean(axis=(0, 1)), want.mean(axis=(0, 1))
-    assert np.all(np.abs(m_got - m_want) <= 0.03 * m_want + 1e-4), (m_got, m_want)
-    if rng == "chacha8":
-        # same random stream: most pixels follow identical paths until an f32 branch flip
+    # both images are means of spp samples: Var(got - want) ~ 2 var / spp for independent streams
+    se_pix = np.sqrt(2.0 * var / spp)
+    for c in range(3):
+        d = got[c::3].mean() - want[c::3].mean()
+        se = np.sqrt(np.sum(2.0 * var[c::3] / spp)) / (w * h)
+        assert abs(d) <= 4.5 * se + 1e-6, (c, d, se)
+    if rng == "philox":
+        # independent streams: compare 4x4-pixel block means (rare light paths make
+        # single-pixel estimates too heavy-tailed at this spp); block z-scores
+        # should look like |N(0,1)| (median 0.674)
+        k = 4
+        def blocks(a):
+            a = a.reshape(h, w, 3)[: h // k * k, : w // k * k]
+            return a.reshape(h // k, k, w // k, k, 3).mean(axis=(1, 3))
+        vb = blocks(2.0 * var / spp) / (k * k)
+        ok = vb > 1e-14
+        z = (blocks(got) - blocks(want))[ok] / np.sqrt(vb[ok])
+        med = float(np.median(np.abs(z)))
+        assert 0.35 <= med <= 1.1, med
+        assert np.mean(np.abs(z) > 5) < 0.03, np.mean(np.abs(z) > 5)
+    else:
+        # same random stream as the reference: many pixels follow identical paths
         close = np.mean(np.abs(got - want) <= 1e-3 + 1e-3 * np.abs(want))
-        assert close >= 0.5, close
+        assert close >= (0.5 if "cornell" in scene else 0.25), close
 
 
 def test_render_device_into_torch_tensor():
-    torch = pytest.importorskip("torch")
+    torch = pytest.importorskip("torch")  # nrt.lib() already imported it first: one HIP runtime
     scene, w, h, spp = "scenes/cornell-box-scene.json", 24, 16, 2
     s = load(scene, w, h, spp)
     ref = s.render(precision="f64", rng="chacha8")
