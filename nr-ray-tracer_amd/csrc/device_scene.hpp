@@ -23,7 +23,11 @@
 
 namespace nrt {
 
-enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2 };
+enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2, NODE_LIST = 3 };
+// NODE_LIST (fast kernel only): a BVH subtree holding only primitives, at most
+// LIST_MAX of them, collapsed into one node: its box is tested, then every
+// primitive in the subtree's depth-first order.  meta = 3 | (count-1) << 2 | first << 8.
+constexpr uint32_t LIST_MAX = 8;
 enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2 };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
@@ -67,8 +71,17 @@ struct alignas(16) DXform {
 struct alignas(16) DInstance {
     uint32_t first_xform;
     uint32_t num_xforms;
-    int32_t root;  // BLAS root node (NODE_END = empty)
-    uint32_t pad;
+    int32_t root;       // BLAS root in the exact node array (NODE_END = empty)
+    int32_t root_fast;  // BLAS root in the fast (list-collapsed) node array
+};
+
+// Fast kernel: an instance's Translate/Rotate/Scale chain composed into one
+// affine map (host, f64, then rounded): object ray o' = A o + b, d' = A d;
+// hit point back p = C p' + c; normal back n = N n' (rotations only, Q11).
+template <typename Real>
+struct alignas(16) DInstFast {
+    Real A[9], b[3], C[9], c[3], N[9];  // 3x3 column major
+    Real pad[3];
 };
 
 struct alignas(16) DMaterial {
@@ -99,6 +112,9 @@ struct DSceneView {
     int32_t root;
     int32_t max_depth;  // deepest instance nesting (0 = no instances)
     uint32_t n_nodes, n_prims, n_xforms, n_instances, n_materials, n_textures;
+    const uint32_t* list_prims;        // fast kernel: primitive ids of NODE_LIST entries
+    const DInstFast<Real>* inst_fast;  // fast kernel: composed instance transforms
+    uint32_t n_list, n_inst_fast;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each
@@ -109,7 +125,8 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
     auto r16 = [](uint64_t b) { return (uint32_t)((b + 15) & ~uint64_t(15)); };
     return r16(v.n_nodes * sizeof(DNode<Real>)) + r16(v.n_prims * sizeof(DPrim<Real>)) +
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
-           r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture));
+           r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
+           r16(v.n_list * sizeof(uint32_t)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>));
 }
 
 }  // namespace nrt

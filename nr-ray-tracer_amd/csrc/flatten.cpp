@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <array>
 #include <deque>
 #include <map>
 #include <stdexcept>
@@ -21,6 +22,8 @@ struct Flattener {
     std::map<const Material*, uint32_t> mat_ids;
     std::map<const Texture*, uint32_t> tex_ids;
     std::map<const Object*, int32_t> blas_roots;          // target object -> tree root
+    std::map<const Object*, uint32_t> inst_ids;           // transform-chain head -> instance
+    std::vector<const Object*> inst_targets;              // instance -> BLAS object
     std::deque<std::pair<uint32_t, const Object*>> pending;  // (instance id, target) to emit
     std::vector<std::pair<uint32_t, uint32_t>> tree_ranges;   // [begin, end) node index per tree
 
@@ -164,23 +167,161 @@ struct Flattener {
             case Object::Translate:
             case Object::Rotate:
             case Object::Scale: {
-                DInstance inst{};
-                inst.first_xform = (uint32_t)out.xforms.size();
-                const Object* t = o;
-                while (is_transform(t)) {
-                    xform(t);
-                    t = t->child.get();
-                }
-                inst.num_xforms = (uint32_t)out.xforms.size() - inst.first_xform;
-                inst.root = NODE_END;
-                const uint32_t iid = (uint32_t)out.instances.size();
-                out.instances.push_back(inst);
-                pending.emplace_back(iid, t);
+                const uint32_t iid = instance(o);
                 const uint32_t idx = push(NODE_INSTANCE, iid);
                 out.nodes[idx].skip = (int32_t)idx + 1;
                 return;
             }
         }
+    }
+
+    // One instance per distinct transform-chain head (a Ref'd chain is shared).
+    uint32_t instance(const Object* o) {
+        auto it = inst_ids.find(o);
+        if (it != inst_ids.end()) return it->second;
+        DInstance inst{};
+        inst.first_xform = (uint32_t)out.xforms.size();
+        const Object* t = o;
+        while (is_transform(t)) {
+            xform(t);
+            t = t->child.get();
+        }
+        inst.num_xforms = (uint32_t)out.xforms.size() - inst.first_xform;
+        inst.root = NODE_END;
+        inst.root_fast = NODE_END;
+        const uint32_t iid = (uint32_t)out.instances.size();
+        out.instances.push_back(inst);
+        out.inst_fast.push_back(compose(inst));
+        inst_targets.push_back(t);
+        pending.emplace_back(iid, t);
+        inst_ids[o] = iid;
+        return iid;
+    }
+
+    // Compose the chain into one affine map each way (f64), for the fast kernel.
+    DInstFast<double> compose(const DInstance& inst) {
+        using Mat = std::array<double, 9>;  // column major
+        auto I = []() { Mat m{}; m[0] = m[4] = m[8] = 1.0; return m; };
+        auto mm = [](const Mat& a, const Mat& b) {  // a * b
+            Mat r{};
+            for (int c = 0; c < 3; ++c)
+                for (int rr = 0; rr < 3; ++rr)
+                    r[3 * c + rr] = a[rr] * b[3 * c] + a[3 + rr] * b[3 * c + 1] + a[6 + rr] * b[3 * c + 2];
+            return r;
+        };
+        auto mv = [](const Mat& a, const std::array<double, 3>& v) {
+            return std::array<double, 3>{a[0] * v[0] + a[3] * v[1] + a[6] * v[2], a[1] * v[0] + a[4] * v[1] + a[7] * v[2],
+                                         a[2] * v[0] + a[5] * v[1] + a[8] * v[2]};
+        };
+        Mat A = I(), C = I(), N = I();
+        std::array<double, 3> b{0, 0, 0}, c{0, 0, 0};
+        for (uint32_t k = 0; k < inst.num_xforms; ++k) {  // world -> object, outer first
+            const DXform<double>& x = out.xforms[inst.first_xform + k];
+            if (x.kind == XF_TRANSLATE) {
+                for (int r = 0; r < 3; ++r) b[r] -= x.m[r];
+            } else {
+                Mat L;
+                for (int q = 0; q < 9; ++q) L[q] = x.m[q];
+                A = mm(L, A);
+                b = mv(L, b);
+                if (x.kind == XF_SCALE)
+                    for (int r = 0; r < 3; ++r) b[r] += x.m[9 + r];
+            }
+        }
+        for (uint32_t k = inst.num_xforms; k-- > 0;) {  // object -> world, inner first
+            const DXform<double>& x = out.xforms[inst.first_xform + k];
+            if (x.kind == XF_TRANSLATE) {
+                for (int r = 0; r < 3; ++r) c[r] += x.m[r];
+            } else {
+                Mat L;
+                for (int q = 0; q < 9; ++q) L[q] = x.inv[q];
+                C = mm(L, C);
+                c = mv(L, c);
+                if (x.kind == XF_SCALE)
+                    for (int r = 0; r < 3; ++r) c[r] += x.inv[9 + r];
+                else
+                    N = mm(L, N);  // only rotations turn the normal (Q11)
+            }
+        }
+        DInstFast<double> f{};
+        for (int q = 0; q < 9; ++q) { f.A[q] = A[q]; f.C[q] = C[q]; f.N[q] = N[q]; }
+        for (int r = 0; r < 3; ++r) { f.b[r] = b[r]; f.c[r] = c[r]; }
+        return f;
+    }
+
+    // ---- fast node array: prim-only subtrees with <= LIST_MAX leaves become NODE_LIST
+    static bool prims_only(const Object* o, uint32_t& n) {
+        switch (o->kind) {
+            case Object::BvhEmpty: return true;
+            case Object::BvhLeaf: return prims_only(o->child.get(), n);
+            case Object::BvhNode: return prims_only(o->left.get(), n) && prims_only(o->right.get(), n);
+            case Object::Sphere:
+            case Object::Quad:
+            case Object::Triangle: ++n; return true;
+            default: return false;
+        }
+    }
+    void collect_prims(const Object* o) {
+        switch (o->kind) {
+            case Object::BvhLeaf: collect_prims(o->child.get()); return;
+            case Object::BvhNode: collect_prims(o->left.get()); collect_prims(o->right.get()); return;
+            case Object::Sphere:
+            case Object::Quad:
+            case Object::Triangle: out.list_prims.push_back(prim(o, o->material)); return;
+            default: return;
+        }
+    }
+    uint32_t push_fast(uint32_t meta) {
+        DNode<double> n{};
+        n.meta = meta;
+        n.skip = NODE_END;
+        out.nodes_fast.push_back(n);
+        return (uint32_t)out.nodes_fast.size() - 1;
+    }
+    void emit_fast(const Object* o) {
+        switch (o->kind) {
+            case Object::BvhEmpty: return;
+            case Object::BvhLeaf: emit_fast(o->child.get()); return;
+            case Object::BvhNode: {
+                uint32_t count = 0;
+                const bool list = prims_only(o, count) && count >= 2 && count <= LIST_MAX;
+                const uint32_t first = (uint32_t)out.list_prims.size();
+                const uint32_t idx = push_fast(list ? (NODE_LIST | ((count - 1) << 2) | (first << 8)) : NODE_INNER);
+                DNode<double>& n = out.nodes_fast[idx];
+                n.bmin[0] = o->bbox.x.min; n.bmax[0] = o->bbox.x.max;
+                n.bmin[1] = o->bbox.y.min; n.bmax[1] = o->bbox.y.max;
+                n.bmin[2] = o->bbox.z.min; n.bmax[2] = o->bbox.z.max;
+                if (list) {
+                    if (first >= (1u << 24)) throw std::runtime_error("too many list entries");
+                    collect_prims(o);
+                } else {
+                    emit_fast(o->left.get());
+                    emit_fast(o->right.get());
+                }
+                out.nodes_fast[idx].skip = (int32_t)out.nodes_fast.size();
+                return;
+            }
+            case Object::Sphere:
+            case Object::Quad:
+            case Object::Triangle: {
+                const uint32_t idx = push_fast(NODE_PRIM | (prim(o, o->material) << 2));
+                out.nodes_fast[idx].skip = (int32_t)idx + 1;
+                return;
+            }
+            default: {
+                const uint32_t idx = push_fast(NODE_INSTANCE | (instance(o) << 2));
+                out.nodes_fast[idx].skip = (int32_t)idx + 1;
+                return;
+            }
+        }
+    }
+    int32_t tree_fast(const Object* o) {
+        const uint32_t begin = (uint32_t)out.nodes_fast.size();
+        emit_fast(o);
+        const uint32_t end = (uint32_t)out.nodes_fast.size();
+        for (uint32_t k = begin; k < end; ++k)
+            if (out.nodes_fast[k].skip == (int32_t)end) out.nodes_fast[k].skip = NODE_END;
+        return end > begin ? (int32_t)begin : NODE_END;
     }
 
     int32_t tree(const Object* o) {
@@ -222,6 +363,16 @@ struct Flattener {
             if (it == blas_roots.end()) it = blas_roots.emplace(target, tree(target)).first;
             out.instances[iid].root = it->second;
         }
+        // fast node array over the same instances
+        out.root_fast = tree_fast(top);
+        std::map<const Object*, int32_t> fast_roots;
+        for (size_t iid = 0; iid < out.instances.size(); ++iid) {
+            const Object* target = inst_targets[iid];
+            auto it = fast_roots.find(target);
+            if (it == fast_roots.end()) it = fast_roots.emplace(target, tree_fast(target)).first;
+            out.instances[iid].root_fast = it->second;
+        }
+        if (!pending.empty()) throw std::runtime_error("internal: instance discovered only by the fast pass");
         std::map<int32_t, int> memo;
         out.max_depth = depth_of(out.root, memo, 0);
         if (out.max_depth > MAX_INSTANCE_DEPTH)
@@ -252,14 +403,21 @@ FlatScene flatten_scene(const ObjectPtr& top) {
 
 FlatScene32 to_f32(const FlatScene& s) {
     FlatScene32 o;
-    o.nodes.resize(s.nodes.size());
-    for (size_t i = 0; i < s.nodes.size(); ++i) {
+    o.nodes.resize(s.nodes_fast.size());
+    for (size_t i = 0; i < s.nodes_fast.size(); ++i) {
         for (int k = 0; k < 3; ++k) {
-            o.nodes[i].bmin[k] = round_down(s.nodes[i].bmin[k]);
-            o.nodes[i].bmax[k] = round_up(s.nodes[i].bmax[k]);
+            o.nodes[i].bmin[k] = round_down(s.nodes_fast[i].bmin[k]);
+            o.nodes[i].bmax[k] = round_up(s.nodes_fast[i].bmax[k]);
         }
-        o.nodes[i].meta = s.nodes[i].meta;
-        o.nodes[i].skip = s.nodes[i].skip;
+        o.nodes[i].meta = s.nodes_fast[i].meta;
+        o.nodes[i].skip = s.nodes_fast[i].skip;
+    }
+    o.inst_fast.resize(s.inst_fast.size());
+    for (size_t i = 0; i < s.inst_fast.size(); ++i) {
+        const auto& a = s.inst_fast[i];
+        auto& b = o.inst_fast[i];
+        for (int q = 0; q < 9; ++q) { b.A[q] = (float)a.A[q]; b.C[q] = (float)a.C[q]; b.N[q] = (float)a.N[q]; }
+        for (int r = 0; r < 3; ++r) { b.b[r] = (float)a.b[r]; b.c[r] = (float)a.c[r]; b.pad[r] = 0.f; }
     }
     o.prims.resize(s.prims.size());
     for (size_t i = 0; i < s.prims.size(); ++i) {

@@ -10,7 +10,11 @@
 namespace nrt {
 
 struct FlatScene {
-    std::vector<DNode<double>> nodes;
+    std::vector<DNode<double>> nodes;       // exact kernel: the reference's BVH node for node
+    std::vector<DNode<double>> nodes_fast;  // fast kernel: small prim-only subtrees -> NODE_LIST
+    std::vector<uint32_t> list_prims;
+    std::vector<DInstFast<double>> inst_fast;
+    int32_t root_fast = NODE_END;
     std::vector<DPrim<double>> prims;
     std::vector<DXform<double>> xforms;
     std::vector<DInstance> instances;
@@ -27,9 +31,10 @@ FlatScene flatten_scene(const ObjectPtr& top_level_bvh);
 // Precision conversion for the fast kernel.  Boxes are rounded outward so an
 // f32 box always contains the f64 one.
 struct FlatScene32 {
-    std::vector<DNode<float>> nodes;
+    std::vector<DNode<float>> nodes;  // from nodes_fast
     std::vector<DPrim<float>> prims;
     std::vector<DXform<float>> xforms;
+    std::vector<DInstFast<float>> inst_fast;
 };
 FlatScene32 to_f32(const FlatScene& s);
 

@@ -375,6 +375,19 @@ __device__ __forceinline__ void xform_out(const DSceneView<R>& sc, const DInstan
     }
 }
 
+// Fast kernel: composed instance map (device_scene.hpp DInstFast)
+template <typename R>
+__device__ __forceinline__ void enter_fast(const DInstFast<R>& f, Ray<R>& r) {
+    r.o = mat3(f.A, r.o) + ld3(f.b);
+    r.d = mat3(f.A, r.d);
+    r.inv = mk(R(1) / r.d.x, R(1) / r.d.y, R(1) / r.d.z);
+}
+template <typename R>
+__device__ __forceinline__ void leave_fast(const DInstFast<R>& f, Rec<R>& h) {
+    h.p = mat3(f.C, h.p) + ld3(f.c);
+    h.n = mat3(f.N, h.n);
+}
+
 template <typename R, int MAXD>
 struct HitMin {
     R t;
@@ -424,9 +437,9 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
             }
             continue;
         }
-        const uint32_t idx = meta >> 2;
-        if ((meta & 3u) == NODE_PRIM) {
-            const DPrim<R>& pr = sc.prims[idx];
+        const uint32_t kind = meta & 3u;
+        auto test_prim = [&](uint32_t pid) {
+            const DPrim<R>& pr = sc.prims[pid];
             R t;
             if (pr.kind == PRIM_SPHERE) {
                 t = sphere_t(pr, ray);
@@ -437,7 +450,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
             }
             if (t >= R(0) && t <= t_best) {
                 t_best = t;
-                hm.prim = idx;
+                hm.prim = pid;
                 hm.depth = depth;
                 if constexpr (MAXD == 1) {
                     hm.inst[0] = inst0;
@@ -447,8 +460,20 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
                 }
                 found = true;
             }
+        };
+        if (kind == NODE_PRIM) {
+            test_prim(meta >> 2);
+            node = skip;
+        } else if (!EXACT && kind == NODE_LIST) {
+            // collapsed prim-only subtree: its box, then its prims in depth-first order
+            const DNode<R>& n = sc.nodes[node];
+            if (box_hit<R, EXACT>(n.bmin, n.bmax, ray, t_best)) {
+                const uint32_t first = meta >> 8, cnt = ((meta >> 2) & 63u) + 1u;
+                for (uint32_t k = 0; k < cnt; ++k) test_prim(sc.list_prims[first + k]);
+            }
             node = skip;
         } else {
+            const uint32_t idx = meta >> 2;
             const DInstance inst = sc.instances[idx];
             if constexpr (MAXD == 1) {
                 ret0 = skip;
@@ -459,8 +484,13 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
                 saved[depth] = ray;
             }
             ++depth;
-            xform_in<R, EXACT>(sc, inst, ray);
-            node = inst.root;
+            if constexpr (EXACT) {
+                xform_in<R, EXACT>(sc, inst, ray);
+                node = inst.root;
+            } else {
+                enter_fast(sc.inst_fast[idx], ray);
+                node = inst.root_fast;
+            }
         }
     }
     hm.t = t_best;
@@ -472,10 +502,18 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
 template <typename R, int MAXD, bool EXACT>
 __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
     Ray<R> ray = wray;
+    auto enter = [&](uint32_t iid) {
+        if constexpr (EXACT) xform_in<R, true>(sc, sc.instances[iid], ray);
+        else enter_fast(sc.inst_fast[iid], ray);
+    };
+    auto leave = [&](uint32_t iid, Rec<R>& rec) {
+        if constexpr (EXACT) xform_out(sc, sc.instances[iid], rec);
+        else leave_fast(sc.inst_fast[iid], rec);
+    };
     if constexpr (MAXD == 1) {
-        if (hm.depth > 0) xform_in<R, true>(sc, sc.instances[hm.inst[0]], ray);
+        if (hm.depth > 0) enter(hm.inst[0]);
     } else {
-        for (int l = 0; l < hm.depth; ++l) xform_in<R, true>(sc, sc.instances[hm.inst[l]], ray);
+        for (int l = 0; l < hm.depth; ++l) enter(hm.inst[l]);
     }
     const DPrim<R>& pr = sc.prims[hm.prim];
     Rec<R> h;
@@ -502,9 +540,9 @@ __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray
     h.n = (-sign) * outward;
     h.mat = pr.material;
     if constexpr (MAXD == 1) {
-        if (hm.depth > 0) xform_out(sc, sc.instances[hm.inst[0]], h);
+        if (hm.depth > 0) leave(hm.inst[0], h);
     } else {
-        for (int l = hm.depth - 1; l >= 0; --l) xform_out(sc, sc.instances[hm.inst[l]], h);
+        for (int l = hm.depth - 1; l >= 0; --l) leave(hm.inst[l], h);
     }
     return h;
 }
@@ -574,6 +612,9 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.instances = (const DInstance*)copy(g.instances, g.n_instances * (uint32_t)sizeof(DInstance));
     s.materials = (const DMaterial*)copy(g.materials, g.n_materials * (uint32_t)sizeof(DMaterial));
     s.textures = (const DTexture*)copy(g.textures, g.n_textures * (uint32_t)sizeof(DTexture));
+    if (g.n_list) s.list_prims = (const uint32_t*)copy(g.list_prims, g.n_list * (uint32_t)sizeof(uint32_t));
+    if (g.n_inst_fast)
+        s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
     __syncthreads();
     return s;
 }

@@ -1,0 +1,57 @@
+"""Summarise rocprofv3 kernel-trace + PMC CSVs of one profile run (scripts/profile.sh).
+
+usage: python scripts/pmc_summary.py gpurun_out/prof_<tag> [--kernel render_kernel] [--json out.json]
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads half of a wide
+coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is exact for
+16-B-per-lane stores and uncalibrated for the 4-B stores this kernel issues.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="render_kernel")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    out = {}
+    st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if st:
+        for r in csv.DictReader(open(st[0])):
+            if a.kernel in r["Name"]:
+                out["kernel"] = r["Name"]
+                out["calls"] = int(r["Calls"])
+                out["avg_ns"] = float(r["AverageNs"])
+    agg = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(a.dir, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if a.kernel in r.get("Kernel_Name", ""):
+                agg[r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[r["Counter_Name"]].add(r.get("Dispatch_Id", ""))
+    per = {k: v / max(len(disp[k]), 1) for k, v in agg.items()}
+    out["per_dispatch"] = per
+    if "FETCH_SIZE" in per or "WRITE_SIZE" in per:
+        fetch = per.get("FETCH_SIZE", 0.0) * 1024 * 2
+        write = per.get("WRITE_SIZE", 0.0) * 1024
+        out["hbm_bytes_per_launch"] = fetch + write
+        out["hbm_fetch_bytes"] = fetch
+        out["hbm_write_bytes"] = write
+    if "SQ_INSTS_VALU" in per and "SQ_WAVES" in per:
+        out["valu_insts_per_wave"] = per["SQ_INSTS_VALU"] / per["SQ_WAVES"]
+    if "SQ_THREAD_CYCLES_VALU" in per and "SQ_ACTIVE_INST_VALU" in per and per["SQ_ACTIVE_INST_VALU"]:
+        out["valu_lane_utilization"] = per["SQ_THREAD_CYCLES_VALU"] / (64.0 * per["SQ_ACTIVE_INST_VALU"])
+    text = json.dumps(out, indent=1, sort_keys=True)
+    print(text)
+    if a.json:
+        with open(a.json, "w") as fh:
+            fh.write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()

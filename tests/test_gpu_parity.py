@@ -157,3 +157,17 @@ def test_empty_and_degenerate_inputs():
     np.testing.assert_array_equal(img, np.broadcast_to(np.array([0.7, 0.8, 1.0], np.float32), img.shape))
     one = b.finish(b.bvh([b.sphere((0, 0, 0), 0.5, m)]), cam)  # single leaf: no bbox test
     assert np.all(np.isfinite(one.render(precision="f64")))
+
+
+@pytest.mark.parametrize("scene,w,h", [(c[0], c[1], c[2]) for c in CASES_F64[:5]])
+@pytest.mark.parametrize("bounces", [1, 2, 3])
+def test_fast_kernel_follows_exact_paths(scene, w, h, bounces):
+    """The f32 kernel (leaf lists, composed instance transforms) must follow the
+    same paths as the exact kernel on the same ChaCha8 stream: with few bounces
+    any geometry bug shows as whole faces of mismatching pixels, while genuine
+    f32 rounding flips stay rare."""
+    s = load(scene, w, h, 1, bounces)
+    a = s.render(precision="f32", rng="chacha8")
+    b = s.render(precision="f64", rng="chacha8")
+    mismatch = np.mean(np.abs(a - b).max(axis=2) > 1e-3 + 1e-3 * np.abs(b).max(axis=2))
+    assert mismatch <= 0.01, mismatch
