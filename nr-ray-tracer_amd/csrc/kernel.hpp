@@ -13,6 +13,8 @@
 //   RNG   = ChaCha8 per-pixel stream (rand_chacha 0.9, bit-exact with the
 //           reference) or Philox4x32-10 keyed per (pixel, sample, draw)
 //   MAXD  = 1 when instances do not nest (all BASELINE scenes), 4 otherwise.
+#pragma once
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,8 +43,19 @@ template <typename R> __device__ __forceinline__ R dot(V<R> a, V<R> b) { return 
 template <typename R> __device__ __forceinline__ V<R> cross(V<R> a, V<R> b) {
     return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
 }
+// Exact (f64) vs fast (f32) arithmetic helpers: the f32 kernel uses the
+// hardware reciprocal / reciprocal-sqrt (1 ulp), the f64 kernel IEEE division.
+template <typename R> __device__ __forceinline__ R fast_rcp(R x) { return R(1) / x; }
+template <> __device__ __forceinline__ float fast_rcp<float>(float x) { return __builtin_amdgcn_rcpf(x); }
+template <typename R> __device__ __forceinline__ R fast_div(R a, R b) { return a / b; }
+template <> __device__ __forceinline__ float fast_div<float>(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+template <typename R> __device__ __forceinline__ V<R> vdiv(V<R> a, R s) { return a / s; }
+template <> __device__ __forceinline__ V<float> vdiv<float>(V<float> a, float s) { return fast_rcp(s) * a; }
 template <typename R> __device__ __forceinline__ V<R> normalize(V<R> a) {
     return (R(1) / sqrt(dot(a, a))) * a;  // glam: self * self.length().recip()
+}
+template <> __device__ __forceinline__ V<float> normalize<float>(V<float> a) {
+    return __builtin_amdgcn_rsqf(dot(a, a)) * a;
 }
 template <typename R> __device__ __forceinline__ V<R> ld3(const R* p) { return {p[0], p[1], p[2]}; }
 template <typename R> __device__ __forceinline__ V<R> ld3d(const double* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
@@ -227,7 +240,7 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sp
         const V<R> p = mk(x, y, z);
         const R ls = dot(p, p);
         const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
-        if (tiny < ls && ls <= R(1)) return p / ls;
+        if (tiny < ls && ls <= R(1)) return vdiv(p, ls);
     }
 }
 // vector.rs:72-81 — rejection in [-1,1)^2 until |p|^2 < 1, returns p/|p|^2
@@ -237,7 +250,7 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_di
         const R y = Uniform<R>::range(g.next(), R(-1), R(1));
         const V<R> p = mk(x, y, R(0));
         const R ls = dot(p, p);
-        if (ls < R(1)) return p / ls;
+        if (ls < R(1)) return vdiv(p, ls);
     }
 }
 
@@ -251,7 +264,7 @@ struct Ray {
 };
 
 template <typename R, bool EXACT> __device__ __forceinline__ void prep_ray(Ray<R>& r) {
-    if constexpr (!EXACT) r.inv = mk(R(1) / r.d.x, R(1) / r.d.y, R(1) / r.d.z);
+    if constexpr (!EXACT) r.inv = mk(fast_rcp(r.d.x), fast_rcp(r.d.y), fast_rcp(r.d.z));
 }
 
 // AABB::hit (aabb.rs:110-132) with range (0.001, t_max); t_max narrows during
@@ -319,7 +332,7 @@ __device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alph
     const V<R> nrm = ld3(q.n);
     const R denom = dot(nrm, r.d);
     if (fabs(denom) < R(1e-8)) return R(-1);
-    const R t = (q.s - dot(nrm, r.o)) / denom;
+    const R t = fast_div(q.s - dot(nrm, r.o), denom);
     if (!(R(0.001) <= t && t <= R(INFINITY))) return R(-1);
     point = r.o + t * r.d;
     const V<R> ph = point - ld3(q.a);
@@ -380,7 +393,7 @@ template <typename R>
 __device__ __forceinline__ void enter_fast(const DInstFast<R>& f, Ray<R>& r) {
     r.o = mat3(f.A, r.o) + ld3(f.b);
     r.d = mat3(f.A, r.d);
-    r.inv = mk(R(1) / r.d.x, R(1) / r.d.y, R(1) / r.d.z);
+    r.inv = mk(fast_rcp(r.d.x), fast_rcp(r.d.y), fast_rcp(r.d.z));
 }
 template <typename R>
 __device__ __forceinline__ void leave_fast(const DInstFast<R>& f, Rec<R>& h) {

@@ -1,0 +1,20 @@
+// Kernel launchers, one translation unit per numeric contract:
+//   kernels_exact.hip  (f64, -ffp-contract=off: the reference's un-fused arithmetic)
+//   kernels_fast.hip   (f32, -ffp-contract=fast + hardware reciprocals)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_scene.hpp"
+#include "render_params.hpp"
+
+namespace nrt {
+
+void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, bool deep, hipStream_t stream);
+void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, bool deep, hipStream_t stream);
+void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
+                      unsigned long long* d_out);
+
+}  // namespace nrt

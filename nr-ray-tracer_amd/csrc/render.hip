@@ -1,6 +1,8 @@
 // MI355X (gfx950) renderer: kernels live in kernel.hpp; this TU instantiates
 // them and holds the host side (device buffers, launches).  No torch types.
-#include "kernel.hpp"
+#include <hip/hip_runtime.h>
+
+#include "launch.hpp"
 
 #include <mutex>
 #include <stdexcept>
@@ -99,60 +101,23 @@ void gpu_free_scene(DeviceScene* ds) {
 size_t gpu_scene_bytes(const DeviceScene* ds) { return ds ? ds->bytes : 0; }
 int gpu_scene_device(const DeviceScene* ds) { return ds ? ds->device : -1; }
 
-// Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
-constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
-
-template <typename R, class G, int MAXD, bool EXACT>
-static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_t stream) {
-    const uint32_t n = p.pixel_end - p.pixel_begin;
-    const uint32_t blocks = (n + dev::BLOCK - 1) / dev::BLOCK;
-    const uint32_t ring = G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0;
-    const uint32_t scene = lds_scene_bytes(v);
-    if (scene <= LDS_SCENE_LIMIT) {
-        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true>), dim3(blocks), dim3(dev::BLOCK), ring + scene,
-                           stream, p, v);
-    } else {
-        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, false>), dim3(blocks), dim3(dev::BLOCK), ring,
-                           stream, p, v);
-    }
-}
-
 void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng,
                        void* stream_ptr) {
     if (p.pixel_end <= p.pixel_begin) return;
     if (p.width == 0) throw std::runtime_error("width must be > 0");
     hipStream_t stream = (hipStream_t)stream_ptr;
     const bool deep = ds->v64.max_depth > 1;
-    if (precision == 0) {
-        if (rng == RNG_CHACHA8) {
-            if (deep) launch_one<double, dev::ChaCha8, MAX_INSTANCE_DEPTH, true>(p, ds->v64, stream);
-            else launch_one<double, dev::ChaCha8, 1, true>(p, ds->v64, stream);
-        } else {
-            if (deep) launch_one<double, dev::Philox, MAX_INSTANCE_DEPTH, true>(p, ds->v64, stream);
-            else launch_one<double, dev::Philox, 1, true>(p, ds->v64, stream);
-        }
-    } else {
-        if (rng == RNG_CHACHA8) {
-            if (deep) launch_one<float, dev::ChaCha8, MAX_INSTANCE_DEPTH, false>(p, ds->v32, stream);
-            else launch_one<float, dev::ChaCha8, 1, false>(p, ds->v32, stream);
-        } else {
-            if (deep) launch_one<float, dev::Philox, MAX_INSTANCE_DEPTH, false>(p, ds->v32, stream);
-            else launch_one<float, dev::Philox, 1, false>(p, ds->v32, stream);
-        }
-    }
+    if (precision == 0) launch_exact(p, ds->v64, rng, deep, stream);
+    else launch_fast(p, ds->v32, rng, deep, stream);
     check(hipGetLastError(), "render kernel launch");
 }
 
 void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out) {
-    if (lanes == 0 || lanes > (uint32_t)dev::BLOCK) throw std::runtime_error("lanes must be in [1, 256]");
+    if (lanes == 0 || lanes > 256u) throw std::runtime_error("lanes must be in [1, 256]");
     unsigned long long* d = nullptr;
     const size_t bytes = (size_t)lanes * count * sizeof(unsigned long long);
     check(hipMalloc((void**)&d, bytes ? bytes : 8), "hipMalloc(rng probe)");
-    if (rng == RNG_CHACHA8)
-        hipLaunchKernelGGL(dev::rng_probe_kernel<dev::ChaCha8>, dim3(1), dim3(lanes),
-                           dev::RING * dev::BLOCK * sizeof(uint2), 0, stream0, count, sample, d);
-    else
-        hipLaunchKernelGGL(dev::rng_probe_kernel<dev::Philox>, dim3(1), dim3(lanes), 0, 0, stream0, count, sample, d);
+    launch_rng_probe(rng, stream0, lanes, count, sample, d);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess && bytes) e = hipMemcpy(host_out, d, bytes, hipMemcpyDeviceToHost);
