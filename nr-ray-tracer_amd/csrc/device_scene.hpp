@@ -26,7 +26,8 @@ namespace nrt {
 enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2, NODE_LIST = 3 };
 // NODE_LIST (fast kernel only): a BVH subtree holding only primitives, at most
 // LIST_MAX of them, collapsed into one node: its box is tested, then every
-// primitive in the subtree's depth-first order.  meta = 3 | (count-1) << 2 | first << 8.
+// primitive in the subtree's depth-first order, stored contiguously in the fast
+// primitive array.  meta = 3 | (count-1) << 2 | first << 8.
 constexpr uint32_t LIST_MAX = 8;
 enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2 };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
@@ -54,6 +55,22 @@ struct alignas(16) DPrim {
     Real s;     // sphere: radius           plane: d = normal.p
     uint32_t kind;
     uint32_t material;
+};
+
+// Fast kernel primitive (64 B in f32).  Plane: alpha = (point-p).(v x w),
+// beta = (point-p).(w x u) (scalar triple products of plane.rs:156-157), so
+// A = v x w, a0 = p.A, B = w x u, b0 = p.B are precomputed on the host in f64.
+template <typename Real>
+struct alignas(16) DPrimFast {
+    Real n[3];  // plane: unit normal        sphere: center
+    Real d;     // plane: d = normal.p       sphere: radius
+    Real A[3];  // plane: v x w              sphere: speed
+    Real a0;    // plane: p.A
+    Real B[3];  // plane: w x u
+    Real b0;    // plane: p.B
+    uint32_t kind;
+    uint32_t material;
+    uint32_t pad[2];
 };
 
 template <typename Real>
@@ -112,9 +129,9 @@ struct DSceneView {
     int32_t root;
     int32_t max_depth;  // deepest instance nesting (0 = no instances)
     uint32_t n_nodes, n_prims, n_xforms, n_instances, n_materials, n_textures;
-    const uint32_t* list_prims;        // fast kernel: primitive ids of NODE_LIST entries
+    const DPrimFast<Real>* fprims;     // fast kernel: primitives in list order
     const DInstFast<Real>* inst_fast;  // fast kernel: composed instance transforms
-    uint32_t n_list, n_inst_fast;
+    uint32_t n_fprims, n_inst_fast;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each
@@ -126,7 +143,7 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
     return r16(v.n_nodes * sizeof(DNode<Real>)) + r16(v.n_prims * sizeof(DPrim<Real>)) +
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
-           r16(v.n_list * sizeof(uint32_t)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>));
+           r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>));
 }
 
 }  // namespace nrt

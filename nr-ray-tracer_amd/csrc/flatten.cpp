@@ -261,13 +261,34 @@ struct Flattener {
             default: return false;
         }
     }
+    uint32_t fast_prim(const Object* o) {
+        DPrimFast<double> f{};
+        f.material = material(o->material);
+        if (o->kind == Object::Sphere) {
+            f.kind = PRIM_SPHERE;
+            set3(f.n, o->center);
+            f.d = o->radius;
+            set3(f.A, o->speed);
+        } else {
+            f.kind = o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE;
+            set3(f.n, o->normal);
+            f.d = o->d;
+            const V3 A = cross(o->v, o->w), B = cross(o->w, o->u);
+            set3(f.A, A);
+            set3(f.B, B);
+            f.a0 = dot(o->p, A);
+            f.b0 = dot(o->p, B);
+        }
+        out.fprims.push_back(f);
+        return (uint32_t)out.fprims.size() - 1;
+    }
     void collect_prims(const Object* o) {
         switch (o->kind) {
             case Object::BvhLeaf: collect_prims(o->child.get()); return;
             case Object::BvhNode: collect_prims(o->left.get()); collect_prims(o->right.get()); return;
             case Object::Sphere:
             case Object::Quad:
-            case Object::Triangle: out.list_prims.push_back(prim(o, o->material)); return;
+            case Object::Triangle: fast_prim(o); return;
             default: return;
         }
     }
@@ -285,14 +306,14 @@ struct Flattener {
             case Object::BvhNode: {
                 uint32_t count = 0;
                 const bool list = prims_only(o, count) && count >= 2 && count <= LIST_MAX;
-                const uint32_t first = (uint32_t)out.list_prims.size();
+                const uint32_t first = (uint32_t)out.fprims.size();
                 const uint32_t idx = push_fast(list ? (NODE_LIST | ((count - 1) << 2) | (first << 8)) : NODE_INNER);
                 DNode<double>& n = out.nodes_fast[idx];
                 n.bmin[0] = o->bbox.x.min; n.bmax[0] = o->bbox.x.max;
                 n.bmin[1] = o->bbox.y.min; n.bmax[1] = o->bbox.y.max;
                 n.bmin[2] = o->bbox.z.min; n.bmax[2] = o->bbox.z.max;
                 if (list) {
-                    if (first >= (1u << 24)) throw std::runtime_error("too many list entries");
+                    if (first >= (1u << 24)) throw std::runtime_error("too many primitives for the fast layout");
                     collect_prims(o);
                 } else {
                     emit_fast(o->left.get());
@@ -304,7 +325,7 @@ struct Flattener {
             case Object::Sphere:
             case Object::Quad:
             case Object::Triangle: {
-                const uint32_t idx = push_fast(NODE_PRIM | (prim(o, o->material) << 2));
+                const uint32_t idx = push_fast(NODE_PRIM | (fast_prim(o) << 2));
                 out.nodes_fast[idx].skip = (int32_t)idx + 1;
                 return;
             }
@@ -411,6 +432,14 @@ FlatScene32 to_f32(const FlatScene& s) {
         }
         o.nodes[i].meta = s.nodes_fast[i].meta;
         o.nodes[i].skip = s.nodes_fast[i].skip;
+    }
+    o.fprims.resize(s.fprims.size());
+    for (size_t i = 0; i < s.fprims.size(); ++i) {
+        const auto& a = s.fprims[i];
+        auto& b = o.fprims[i];
+        for (int k = 0; k < 3; ++k) { b.n[k] = (float)a.n[k]; b.A[k] = (float)a.A[k]; b.B[k] = (float)a.B[k]; }
+        b.d = (float)a.d; b.a0 = (float)a.a0; b.b0 = (float)a.b0;
+        b.kind = a.kind; b.material = a.material; b.pad[0] = b.pad[1] = 0;
     }
     o.inst_fast.resize(s.inst_fast.size());
     for (size_t i = 0; i < s.inst_fast.size(); ++i) {

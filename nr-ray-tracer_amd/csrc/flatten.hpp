@@ -12,7 +12,7 @@ namespace nrt {
 struct FlatScene {
     std::vector<DNode<double>> nodes;       // exact kernel: the reference's BVH node for node
     std::vector<DNode<double>> nodes_fast;  // fast kernel: small prim-only subtrees -> NODE_LIST
-    std::vector<uint32_t> list_prims;
+    std::vector<DPrimFast<double>> fprims;  // fast kernel primitives, list order
     std::vector<DInstFast<double>> inst_fast;
     int32_t root_fast = NODE_END;
     std::vector<DPrim<double>> prims;
@@ -35,6 +35,7 @@ struct FlatScene32 {
     std::vector<DPrim<float>> prims;
     std::vector<DXform<float>> xforms;
     std::vector<DInstFast<float>> inst_fast;
+    std::vector<DPrimFast<float>> fprims;
 };
 FlatScene32 to_f32(const FlatScene& s);
 

@@ -346,6 +346,29 @@ __device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alph
     return inside ? t : R(-1);
 }
 
+// Fast kernel primitive test, branch-light (one select per condition):
+// returns t in [0.001, t_max] of a hit, else -1.
+template <typename R>
+__device__ __forceinline__ R fast_prim_t(const DPrimFast<R>& q, const Ray<R>& r, R t_max) {
+    if (q.kind == PRIM_SPHERE) {
+        DPrim<R> s;
+        for (int k = 0; k < 3; ++k) { s.a[k] = q.n[k]; s.b[k] = q.A[k]; }
+        s.s = q.d;
+        const R t = sphere_t(s, r);
+        return t <= t_max ? t : R(-1);
+    }
+    const V<R> n = ld3(q.n);
+    const R denom = dot(n, r.d);
+    const R t = (q.d - dot(n, r.o)) * fast_rcp(denom);
+    const V<R> p = r.o + t * r.d;
+    const R alpha = dot(p, ld3(q.A)) - q.a0;
+    const R beta = dot(p, ld3(q.B)) - q.b0;
+    const bool quad_in = (alpha >= R(0) && alpha <= R(1)) && (beta >= R(0) && beta <= R(1));
+    const bool tri_in = alpha > R(0) && beta > R(0) && (alpha + beta) < R(1);
+    const bool ok = fabs(denom) >= R(1e-8) && t >= R(0.001) && t <= t_max && (q.kind == PRIM_QUAD ? quad_in : tri_in);
+    return ok ? t : R(-1);
+}
+
 // ray into object space through an instance's chain (outer -> inner)
 template <typename R, bool EXACT>
 __device__ __forceinline__ void xform_in(const DSceneView<R>& sc, const DInstance& inst, Ray<R>& r) {
@@ -452,14 +475,18 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
         }
         const uint32_t kind = meta & 3u;
         auto test_prim = [&](uint32_t pid) {
-            const DPrim<R>& pr = sc.prims[pid];
             R t;
-            if (pr.kind == PRIM_SPHERE) {
-                t = sphere_t(pr, ray);
+            if constexpr (EXACT) {
+                const DPrim<R>& pr = sc.prims[pid];
+                if (pr.kind == PRIM_SPHERE) {
+                    t = sphere_t(pr, ray);
+                } else {
+                    R alpha, beta;
+                    V<R> point;
+                    t = plane_t(pr, ray, alpha, beta, point);
+                }
             } else {
-                R alpha, beta;
-                V<R> point;
-                t = plane_t(pr, ray, alpha, beta, point);
+                t = fast_prim_t(sc.fprims[pid], ray, t_best);
             }
             if (t >= R(0) && t <= t_best) {
                 t_best = t;
@@ -482,7 +509,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
             const DNode<R>& n = sc.nodes[node];
             if (box_hit<R, EXACT>(n.bmin, n.bmax, ray, t_best)) {
                 const uint32_t first = meta >> 8, cnt = ((meta >> 2) & 63u) + 1u;
-                for (uint32_t k = 0; k < cnt; ++k) test_prim(sc.list_prims[first + k]);
+                for (uint32_t k = 0; k < cnt; ++k) test_prim(first + k);
             }
             node = skip;
         } else {
@@ -528,11 +555,29 @@ __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray
     } else {
         for (int l = 0; l < hm.depth; ++l) enter(hm.inst[l]);
     }
-    const DPrim<R>& pr = sc.prims[hm.prim];
     Rec<R> h;
     V<R> outward;
     const R t = hm.t;
-    if (pr.kind == PRIM_SPHERE) {  // sphere.rs:148-161
+    if constexpr (!EXACT) {
+        const DPrimFast<R>& q = sc.fprims[hm.prim];
+        h.p = ray.o + t * ray.d;
+        if (q.kind == PRIM_SPHERE) {
+            const V<R> center = ld3(q.n) + ray.time * ld3(q.A);
+            outward = normalize(h.p - center);
+            const R theta = acos(-outward.y);
+            const R phi = atan2(-outward.z, outward.x) + R(M_PI);
+            h.u = phi * R(1.0 / (2.0 * M_PI));
+            h.v = theta * R(1.0 / M_PI);
+        } else {
+            h.u = dot(h.p, ld3(q.A)) - q.a0;
+            h.v = dot(h.p, ld3(q.B)) - q.b0;
+            outward = ld3(q.n);
+        }
+        h.mat = q.material;
+    }
+    const DPrim<R>& pr = sc.prims[EXACT ? hm.prim : 0];
+    if (!EXACT) {
+    } else if (pr.kind == PRIM_SPHERE) {  // sphere.rs:148-161
         const V<R> center = ld3(pr.a) + ray.time * ld3(pr.b);
         h.p = ray.o + t * ray.d;
         outward = normalize(h.p - center);
@@ -551,7 +596,7 @@ __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray
     const R sign = signum(dot(ray.d, outward));
     h.front = sign < R(0);
     h.n = (-sign) * outward;
-    h.mat = pr.material;
+    if constexpr (EXACT) h.mat = pr.material;
     if constexpr (MAXD == 1) {
         if (hm.depth > 0) leave(hm.inst[0], h);
     } else {
@@ -625,9 +670,8 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.instances = (const DInstance*)copy(g.instances, g.n_instances * (uint32_t)sizeof(DInstance));
     s.materials = (const DMaterial*)copy(g.materials, g.n_materials * (uint32_t)sizeof(DMaterial));
     s.textures = (const DTexture*)copy(g.textures, g.n_textures * (uint32_t)sizeof(DTexture));
-    if (g.n_list) s.list_prims = (const uint32_t*)copy(g.list_prims, g.n_list * (uint32_t)sizeof(uint32_t));
-    if (g.n_inst_fast)
-        s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
+    s.fprims = (const DPrimFast<R>*)copy(g.fprims, g.n_fprims * (uint32_t)sizeof(DPrimFast<R>));
+    s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
     __syncthreads();
     return s;
 }

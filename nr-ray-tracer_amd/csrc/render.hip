@@ -65,10 +65,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* mats = (DMaterial*)track(upload(fs.materials, "materials"), fs.materials.size() * sizeof(DMaterial));
         auto* texs = (DTexture*)track(upload(fs.textures, "textures"), fs.textures.size() * sizeof(DTexture));
         auto* texels = (float*)track(upload(fs.texels, "texels"), fs.texels.size() * sizeof(float));
-        // LDS staging copies whole 16-byte chunks: pad the 4-byte list to a multiple of 4 entries
-        std::vector<uint32_t> list_padded = fs.list_prims;
-        while (list_padded.size() % 4) list_padded.push_back(0);
-        auto* lists = (uint32_t*)track(upload(list_padded, "list_prims"), list_padded.size() * sizeof(uint32_t));
+        auto* fpr = (DPrimFast<float>*)track(upload(f32.fprims, "fprims"), f32.fprims.size() * sizeof(DPrimFast<float>));
         auto* ifast = (DInstFast<float>*)track(upload(f32.inst_fast, "inst_fast"),
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
@@ -78,9 +75,10 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, 0, 0};
+        // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
-                                    (uint32_t)f32.nodes.size(), np, nx, ni, nm, nt, lists, ifast,
-                                    (uint32_t)list_padded.size(), (uint32_t)f32.inst_fast.size()};
+                                    (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast,
+                                    (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size()};
     } catch (...) {
         gpu_free_scene(ds);
         throw;
