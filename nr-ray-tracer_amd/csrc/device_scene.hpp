@@ -107,6 +107,17 @@ struct alignas(16) DMaterial {
     double param;  // Metal fuzz / Dielectric refraction index / DiffuseLight intensity
 };
 
+// Fast kernel material: parameter in f32 and a solid texture's colour inline
+// (the common case needs one 32-B LDS read per bounce).
+struct alignas(16) DMatFast {
+    uint32_t kind;
+    uint32_t texture;
+    float param;
+    uint32_t solid;  // 1: `color` is the (SolidColor) texture
+    float color[3];
+    float pad;
+};
+
 struct alignas(16) DTexture {
     uint32_t kind;
     uint32_t a, b;     // image: width, height; checker: even, odd texture ids
@@ -131,7 +142,8 @@ struct DSceneView {
     uint32_t n_nodes, n_prims, n_xforms, n_instances, n_materials, n_textures;
     const DPrimFast<Real>* fprims;     // fast kernel: primitives in list order
     const DInstFast<Real>* inst_fast;  // fast kernel: composed instance transforms
-    uint32_t n_fprims, n_inst_fast;
+    const DMatFast* mats_fast;         // fast kernel: materials with inline solid colour
+    uint32_t n_fprims, n_inst_fast, n_mats_fast;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each
@@ -143,7 +155,8 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
     return r16(v.n_nodes * sizeof(DNode<Real>)) + r16(v.n_prims * sizeof(DPrim<Real>)) +
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
-           r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>));
+           r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>)) +
+           r16(v.n_mats_fast * sizeof(DMatFast));
 }
 
 }  // namespace nrt

@@ -394,6 +394,17 @@ struct Flattener {
             out.instances[iid].root_fast = it->second;
         }
         if (!pending.empty()) throw std::runtime_error("internal: instance discovered only by the fast pass");
+        for (const DMaterial& m : out.materials) {
+            DMatFast f{};
+            f.kind = m.kind;
+            f.texture = m.texture;
+            f.param = (float)m.param;
+            if (m.kind != MAT_DIELECTRIC && out.textures[m.texture].kind == TEX_SOLID) {
+                f.solid = 1;
+                for (int k = 0; k < 3; ++k) f.color[k] = (float)out.textures[m.texture].color[k];
+            }
+            out.mats_fast.push_back(f);
+        }
         std::map<int32_t, int> memo;
         out.max_depth = depth_of(out.root, memo, 0);
         if (out.max_depth > MAX_INSTANCE_DEPTH)

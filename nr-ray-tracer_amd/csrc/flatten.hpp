@@ -13,6 +13,7 @@ struct FlatScene {
     std::vector<DNode<double>> nodes;       // exact kernel: the reference's BVH node for node
     std::vector<DNode<double>> nodes_fast;  // fast kernel: small prim-only subtrees -> NODE_LIST
     std::vector<DPrimFast<double>> fprims;  // fast kernel primitives, list order
+    std::vector<DMatFast> mats_fast;
     std::vector<DInstFast<double>> inst_fast;
     int32_t root_fast = NODE_END;
     std::vector<DPrim<double>> prims;

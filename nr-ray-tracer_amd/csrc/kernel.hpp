@@ -187,30 +187,35 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 struct Philox {
     static constexpr bool uses_lds = false;
     uint32_t pix, sample, pair;
-    uint64_t spare;
-    bool has_spare;
+    uint32_t w0, w1, w2, w3;  // unread words of the current block, consumed in order
+    uint32_t left;
     __device__ __forceinline__ void init(uint64_t stream, uint2*) {
         pix = (uint32_t)stream;
         sample = 0;
         pair = 0;
-        has_spare = false;
+        left = 0;
     }
     __device__ __forceinline__ void start_sample(uint32_t s) {
         sample = s;
         pair = 0;
-        has_spare = false;
+        left = 0;
+    }
+    __device__ __forceinline__ uint32_t next32() {
+        if (left == 0) {
+            uint32_t w[4];
+            philox4x32_10(pix, sample, pair, 0u, 0u, 0u, w);
+            ++pair;
+            w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
+            left = 4;
+        }
+        const uint32_t r = w0;
+        w0 = w1; w1 = w2; w2 = w3;
+        --left;
+        return r;
     }
     __device__ __forceinline__ uint64_t next() {
-        if (has_spare) {
-            has_spare = false;
-            return spare;
-        }
-        uint32_t w[4];
-        philox4x32_10(pix, sample, pair, 0u, 0u, 0u, w);
-        ++pair;
-        spare = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-        has_spare = true;
-        return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        const uint32_t lo = next32();
+        return (uint64_t)lo | ((uint64_t)next32() << 32);
     }
 };
 
@@ -231,12 +236,25 @@ template <> struct Uniform<float> {
     }
 };
 
+// One uniform draw in [low, high).  ChaCha8 always consumes a whole u64 (the
+// reference's next_u64) so the f32 kernel keeps the reference's stream; Philox
+// in the f32 kernel spends 32 bits per draw (23 are used), 4 draws per block.
+template <typename R, class G>
+__device__ __forceinline__ R draw(G& g, R low, R high) {
+    if constexpr (sizeof(R) == 4 && !G::uses_lds) {
+        const float v12 = __uint_as_float(0x3F800000u | (g.next32() >> 9));
+        return (v12 - 1.0f) * (high - low) + low;
+    } else {
+        return Uniform<R>::range(g.next(), low, high);
+    }
+}
+
 // vector.rs:61-70 — rejection in [-1,1)^3 until 1e-160 < |p|^2 <= 1, returns p/|p|^2
 template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sphere(G& g) {
     while (true) {
-        const R x = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R y = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R z = Uniform<R>::range(g.next(), R(-1), R(1));
+        const R x = draw<R>(g, R(-1), R(1));
+        const R y = draw<R>(g, R(-1), R(1));
+        const R z = draw<R>(g, R(-1), R(1));
         const V<R> p = mk(x, y, z);
         const R ls = dot(p, p);
         const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
@@ -246,8 +264,8 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sp
 // vector.rs:72-81 — rejection in [-1,1)^2 until |p|^2 < 1, returns p/|p|^2
 template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_disk(G& g) {
     while (true) {
-        const R x = Uniform<R>::range(g.next(), R(-1), R(1));
-        const R y = Uniform<R>::range(g.next(), R(-1), R(1));
+        const R x = draw<R>(g, R(-1), R(1));
+        const R y = draw<R>(g, R(-1), R(1));
         const V<R> p = mk(x, y, R(0));
         const R ls = dot(p, p);
         if (ls < R(1)) return vdiv(p, ls);
@@ -424,6 +442,22 @@ __device__ __forceinline__ void leave_fast(const DInstFast<R>& f, Rec<R>& h) {
     h.n = mat3(f.N, h.n);
 }
 
+// Whole node in one go (16-byte loads issued together, before the kind test).
+template <typename R>
+__device__ __forceinline__ DNode<R> load_node(const DNode<R>* p) {
+    DNode<R> n;
+    const uint4* s = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&n);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(DNode<R>) / 16); ++k) d[k] = s[k];
+    // keep every part live here: otherwise the box loads sink below the kind
+    // test and a second dependent LDS round trip follows the first
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(DNode<R>) / 16); ++k)
+        asm volatile("" ::"v"(d[k].x), "v"(d[k].y), "v"(d[k].z), "v"(d[k].w));
+    return n;
+}
+
 template <typename R, int MAXD>
 struct HitMin {
     R t;
@@ -455,7 +489,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
         uint32_t meta = 0;
         int32_t skip = NODE_END;
         while (node >= 0) {
-            const DNode<R>& n = sc.nodes[node];
+            const DNode<R> n = load_node(sc.nodes + node);  // one fetch: box + links
             meta = n.meta;
             skip = n.skip;
             if ((meta & 3u) != NODE_INNER) break;
@@ -672,6 +706,7 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.textures = (const DTexture*)copy(g.textures, g.n_textures * (uint32_t)sizeof(DTexture));
     s.fprims = (const DPrimFast<R>*)copy(g.fprims, g.n_fprims * (uint32_t)sizeof(DPrimFast<R>));
     s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
+    s.mats_fast = (const DMatFast*)copy(g.mats_fast, g.n_mats_fast * (uint32_t)sizeof(DMatFast));
     __syncthreads();
     return s;
 }
@@ -716,14 +751,14 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
             // Camera::get_ray (camera.rs:244-267)
             R ox = R(0), oy = R(0);
             if (p.spp > 1) {
-                ox = Uniform<R>::range(g.next(), R(-0.5), R(0.5));
-                oy = Uniform<R>::range(g.next(), R(-0.5), R(0.5));
+                ox = draw<R>(g, R(-0.5), R(0.5));
+                oy = draw<R>(g, R(-0.5), R(0.5));
             }
             const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
             const V<R> disk = random_in_unit_disk<R>(g);
             ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
             ray.d = point - ray.o;
-            ray.time = Uniform<R>::range(g.next(), R(0.0), R(1.0));
+            ray.time = draw<R>(g, R(0.0), R(1.0));
             prep_ray<R, EXACT>(ray);
             tp = mk(R(1), R(1), R(1));
             b = 0;
@@ -739,32 +774,49 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
                 contrib = tp * background;
             } else {
                 const Rec<R> h = make_record<R, MAXD, EXACT>(sc, ray, hm);
-                const DMaterial m = sc.materials[h.mat];
-                if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
-                    const R k = bounced ? (R)m.param : R(1.0);
-                    contrib = tp * (k * tex_color(sc, m.texture, h.u, h.v));
+                uint32_t mkind, mtex;
+                R mparam;
+                bool msolid = false;
+                V<R> mcolor;
+                if constexpr (EXACT) {
+                    const DMaterial m = sc.materials[h.mat];
+                    mkind = m.kind;
+                    mtex = m.texture;
+                    mparam = (R)m.param;
+                } else {
+                    const DMatFast m = sc.mats_fast[h.mat];
+                    mkind = m.kind;
+                    mtex = m.texture;
+                    mparam = m.param;
+                    msolid = m.solid != 0;
+                    mcolor = mk(m.color[0], m.color[1], m.color[2]);
+                }
+                auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
+                if (mkind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
+                    const R k = bounced ? mparam : R(1.0);
+                    contrib = tp * (k * albedo());
                 } else {
                     V<R> dir;
                     V<R> att = mk(R(1), R(1), R(1));
                     bool scattered = true;
-                    if (m.kind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
-                        const R ri = h.front ? R(1.0) / (R)m.param : (R)m.param;
+                    if (mkind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
+                        const R ri = h.front ? R(1.0) / mparam : mparam;
                         const V<R> unit = normalize(ray.d);
                         const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
                         const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
                         bool refl = ri * sin_theta > R(1.0);
-                        if (!refl) refl = reflectance(cos_theta, ri) > Uniform<R>::range(g.next(), R(0.0), R(1.0));
+                        if (!refl) refl = reflectance(cos_theta, ri) > draw<R>(g, R(0.0), R(1.0));
                         dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
                     } else {
                         const V<R> rs = random_in_unit_sphere<R>(g);
-                        if (m.kind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
+                        if (mkind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
                             dir = h.n + rs;
                             if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
                         } else {  // metal.rs:73-91 (draws even when fuzz = 0, Q5)
-                            dir = normalize(reflect(ray.d, h.n)) + (R)m.param * rs;
+                            dir = normalize(reflect(ray.d, h.n)) + mparam * rs;
                             scattered = dot(dir, h.n) > R(0.0);  // else absorbed: emitted = 0
                         }
-                        if (scattered) att = tex_color(sc, m.texture, h.u, h.v);
+                        if (scattered) att = albedo();
                     }
                     if (scattered) {
                         tp = tp * att;

@@ -68,17 +68,19 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* fpr = (DPrimFast<float>*)track(upload(f32.fprims, "fprims"), f32.fprims.size() * sizeof(DPrimFast<float>));
         auto* ifast = (DInstFast<float>*)track(upload(f32.inst_fast, "inst_fast"),
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
+        auto* mfast = (DMatFast*)track(upload(fs.mats_fast, "mats_fast"), fs.mats_fast.size() * sizeof(DMatFast));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
                        ni = (uint32_t)fs.instances.size(), nm = (uint32_t)fs.materials.size(),
                        nt = (uint32_t)fs.textures.size();
         // f64 view: the exact node array (reference node for node); f32 view: the
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
-                                     (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, 0, 0};
+                                     (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
-                                    (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast,
-                                    (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size()};
+                                    (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
+                                    (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
+                                    (uint32_t)fs.mats_fast.size()};
     } catch (...) {
         gpu_free_scene(ds);
         throw;
