@@ -198,6 +198,7 @@ void* device_alloc(size_t bytes, int device);
 void device_free(void* p, int device);
 void device_copy_to_host(void* dst, const void* src, size_t bytes, int device);
 void device_sync(int device);
+void device_zero(void* p, size_t bytes, int device);
 }
 }
 
@@ -464,6 +465,38 @@ int nrt_image_to_rgb8(const float* rgb, size_t n, float gamma, uint8_t* out) {
             const float c = !(g < 1.0f) ? 1.0f : std::fmax(g, 0.0f);  // image crate normalize_float
             out[k] = (uint8_t)std::nearbyint(std::round(c * 255.0f));
         }
+        return NRT_OK;
+    });
+}
+
+int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
+                            uint64_t* out, size_t n) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!scene || !camera || !out || n < 5) throw std::invalid_argument("need scene, camera and out[5]");
+        check_opts(opts);
+        const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
+        RenderParams p = make_params(*camera, opts, rows);
+        const size_t floats = (size_t)rows * p.width * 3;
+        const int dev = resolve_device(opts);
+        DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
+        void* img = device_alloc(floats * sizeof(float) + 64, dev);
+        void* ctr = device_alloc(8 * sizeof(uint64_t), dev);
+        try {
+            device_zero(ctr, 8 * sizeof(uint64_t), dev);
+            p.out = (float*)img;
+            p.counters = (unsigned long long*)ctr;
+            gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, nullptr);
+            device_sync(dev);
+            uint64_t h[8];
+            device_copy_to_host(h, ctr, sizeof h, dev);
+            for (size_t k = 0; k < 5; ++k) out[k] = h[k];
+        } catch (...) {
+            device_free(img, dev);
+            device_free(ctr, dev);
+            throw;
+        }
+        device_free(img, dev);
+        device_free(ctr, dev);
         return NRT_OK;
     });
 }

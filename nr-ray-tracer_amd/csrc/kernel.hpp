@@ -716,9 +716,23 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // sample as soon as its current path terminates, so a wave no longer waits for
 // its longest path every sample; each lane still consumes its pixel's RNG
 // stream strictly in sample order and sums samples in order (camera.rs:325-331).
-template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE>
+//
+// PROF (diagnostic builds only, never timed): per-wave s_memtime stamps split
+// each loop iteration into camera-ray / trace / shading cycles, summed into
+// p.counters[0..3] = {iterations, camera, trace, shade} (+ [4] waves).
+template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF = false>
 __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][4];
+    if constexpr (PROF) {
+        if (threadIdx.x < (BLOCK / 64) * 4) prof[threadIdx.x / 4][threadIdx.x % 4] = 0;
+        __syncthreads();
+    }
+    const uint32_t wave = threadIdx.x / 64;
+    auto stamp = [&]() -> unsigned long long { return PROF ? __builtin_amdgcn_s_memtime() : 0ull; };
+    auto leader = [&]() {  // first active lane of the wave
+        return (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x;
+    };
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes);
@@ -744,6 +758,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
     Ray<R> ray;
     V<R> tp = mk(R(1), R(1), R(1));
     while (true) {
+        const unsigned long long t0 = stamp();
         if (fresh) {
             if (s >= p.spp) break;
             g.start_sample(s);
@@ -765,12 +780,16 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
             bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
             fresh = false;
         }
+        const unsigned long long t1 = stamp();
+        unsigned long long t2 = t1;
         // one step of get_ray_color (camera.rs:269-300): L = a0*(a1*(...*T))
         bool term = true;
         V<R> contrib = mk(R(0), R(0), R(0));
         if (b < p.max_bounces) {  // depth cap returns black (Q6)
             HitMin<R, MAXD> hm;
-            if (!trace<R, MAXD, EXACT>(sc, ray, hm)) {
+            const bool hit = trace<R, MAXD, EXACT>(sc, ray, hm);
+            t2 = stamp();
+            if (!hit) {
                 contrib = tp * background;
             } else {
                 const Rec<R> h = make_record<R, MAXD, EXACT>(sc, ray, hm);
@@ -835,6 +854,21 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
             ay += (double)contrib.y;
             az += (double)contrib.z;
             fresh = true;
+        }
+        if constexpr (PROF) {
+            const unsigned long long t3 = stamp();
+            if (leader()) {
+                atomicAdd(&prof[wave][0], 1ull);
+                atomicAdd(&prof[wave][1], t1 - t0);
+                atomicAdd(&prof[wave][2], t2 - t1);
+                atomicAdd(&prof[wave][3], t3 - t2);
+            }
+        }
+    }
+    if constexpr (PROF) {
+        if (leader()) {
+            for (int c = 0; c < 4; ++c) atomicAdd(&p.counters[c], prof[wave][c]);
+            atomicAdd(&p.counters[4], 1ull);
         }
     }
     const double spp = (double)p.spp;

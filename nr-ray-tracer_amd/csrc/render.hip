@@ -142,6 +142,10 @@ void device_copy_to_host(void* dst, const void* src, size_t bytes, int device) {
     check(hipSetDevice(device), "hipSetDevice");
     check(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy(output)");
 }
+void device_zero(void* p, size_t bytes, int device) {
+    check(hipSetDevice(device), "hipSetDevice");
+    check(hipMemset(p, 0, bytes), "hipMemset");
+}
 void device_sync(int device) {
     check(hipSetDevice(device), "hipSetDevice");
     check(hipDeviceSynchronize(), "render kernel");

@@ -113,6 +113,8 @@ SIGNATURES = {
     "nrt_image_to_rgb8": (C.c_int, [C.POINTER(C.c_float), C.c_size_t, C.c_float, C.POINTER(C.c_uint8)]),
     "nrt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(C.c_uint64)]),
+    "nrt_debug_phase_profile": (C.c_int, [C.c_void_p, C.POINTER(_Camera), C.POINTER(_RenderOpts),
+                                          C.POINTER(C.c_uint64), C.c_size_t]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -346,6 +348,19 @@ class Scene:
         _check(lib().nrt_render(self._h, C.byref(cam._c()), C.byref(o),
                                 out.ctypes.data_as(C.POINTER(C.c_float)), out.size, cb, None))
         return out
+
+    def phase_profile(self, camera: Optional[Camera] = None, precision: str = "f32", rng: str = "philox",
+                      device: int = -1) -> dict:
+        """Diagnostic render with per-wave stamps: cycle shares of camera / trace / shading."""
+        cam = camera or self.camera
+        o = _opts(precision, rng, device, 0, 1)
+        out = (C.c_uint64 * 5)()
+        _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 5))
+        iters, cam_c, trace_c, shade_c, waves = list(out)
+        tot = max(cam_c + trace_c + shade_c, 1)
+        return {"iterations_per_wave": iters / max(waves, 1), "camera_share": cam_c / tot,
+                "trace_share": trace_c / tot, "shade_share": shade_c / tot,
+                "cycles_per_iteration": tot / max(iters, 1), "waves": waves}
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",
                       rng: str = "philox", device: int = -1, row_offset: int = 0, row_stride: int = 1,
