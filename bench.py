@@ -101,7 +101,7 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--rng", default="chacha8", choices=["chacha8", "philox"])
+    ap.add_argument("--rng", default="philox", choices=["chacha8", "philox"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)
     args = ap.parse_args()
