@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--rng", default="philox", choices=["chacha8", "philox"])
+    ap.add_argument("--trace", default="auto", choices=["auto", "bvh", "world-list"],
+                    help="f32 kernel traversal (nrt_trace): auto = world-space list for small flattenable scenes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)
     args = ap.parse_args()
@@ -148,7 +150,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         scene.render_device(buf.data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng, device=local,
-                            row_offset=rank, row_stride=world, stream=stream.cuda_stream)
+                            row_offset=rank, row_stride=world, stream=stream.cuda_stream, trace=args.trace)
         e1.record(stream)
         if timed:
             ev.append((e0, e1))
@@ -189,7 +191,8 @@ def main():
             "data": "reference scene file scenes/cornell-box-scene.json (no dataset; scene is the input)",
             "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} spp={spp}", "scene": args.scene,
                        "width": W, "height": H, "spp": spp, "ray_max_bounces": cam.ray_max_bounces,
-                       "rng": args.rng, "precision": args.precision,
+                       "rng": args.rng, "precision": args.precision, "trace": args.trace,
+                       "world_prims": st["world_prims"],
                        "parallelism": f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -34,6 +34,12 @@ enum {
 
 enum nrt_precision { NRT_PRECISION_F64 = 0, NRT_PRECISION_F32 = 1 };
 enum nrt_rng { NRT_RNG_CHACHA8 = 0, NRT_RNG_PHILOX = 1 };
+/* Traversal of the f32 kernel (the f64 kernel always walks the reference's BVH):
+ * AUTO picks WORLD_LIST for scenes whose primitives all flatten to world space
+ * and number at most NRT_WORLD_LIST_MAX, else BVH (instances kept, per-lane
+ * traversal).  WORLD_LIST fails with NRT_E_INVALID on scenes that cannot flatten. */
+enum nrt_trace { NRT_TRACE_AUTO = 0, NRT_TRACE_BVH = 1, NRT_TRACE_WORLD_LIST = 2 };
+#define NRT_WORLD_LIST_MAX 48
 
 typedef struct nrt_scene nrt_scene;
 typedef struct nrt_builder nrt_builder;
@@ -107,13 +113,15 @@ typedef struct {
     int32_t device;      /* HIP device ordinal; -1 = current device */
     uint32_t row_offset; /* render image rows y = row_offset + k*row_stride ... */
     uint32_t row_stride; /* ... (0 or 1: every row); output rows are compact */
-    uint32_t reserved[3];
+    uint32_t trace;      /* nrt_trace (f32 kernel only) */
+    uint32_t reserved[2];
 } nrt_render_opts;
 
 typedef struct {
     uint64_t nodes, prims, instances, xforms, materials, textures, texels;
     uint32_t trees, max_instance_depth;
     uint64_t device_bytes; /* HBM bytes of the flattened scene on one device */
+    uint64_t world_prims;  /* primitives after flattening instances to world space (0: not flattenable) */
 } nrt_scene_stats;
 
 typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);

@@ -187,6 +187,7 @@ void check_opts(const nrt_render_opts* o) {
     if (!o) return;
     if (o->precision > NRT_PRECISION_F32) throw std::invalid_argument("unknown precision");
     if (o->rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
+    if (o->trace > NRT_TRACE_WORLD_LIST) throw std::invalid_argument("unknown trace mode");
 }
 
 }  // namespace
@@ -375,7 +376,7 @@ int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nr
         const int dev = resolve_device(opts);
         DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
         p.out = dev_out_rgb;
-        gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, hip_stream);
+        gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, opts ? opts->trace : 0, hip_stream);
         return NRT_OK;
     });
 }
@@ -402,7 +403,7 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
                 p.pixel_begin = c * per;
                 p.pixel_end = std::min(total, (c + 1) * per);
                 if (p.pixel_begin >= p.pixel_end) break;
-                gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, nullptr);
+                gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, opts ? opts->trace : 0, nullptr);
                 if (progress) {
                     device_sync(dev);
                     progress(user, p.pixel_end);
@@ -436,7 +437,11 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
                             f.prims.size() * (sizeof(DPrim<double>) + sizeof(DPrim<float>)) +
                             f.xforms.size() * (sizeof(DXform<double>) + sizeof(DXform<float>)) +
                             f.instances.size() * sizeof(DInstance) + f.materials.size() * sizeof(DMaterial) +
-                            f.textures.size() * sizeof(DTexture) + f.texels.size() * sizeof(float);
+                            f.textures.size() * sizeof(DTexture) + f.texels.size() * sizeof(float) +
+                            f.nodes_fast.size() * sizeof(DNode<float>) + f.fprims.size() * sizeof(DPrimFast<float>) +
+                            f.inst_fast.size() * sizeof(DInstFast<float>) + f.mats_fast.size() * sizeof(DMatFast) +
+                            f.wprims.size() * sizeof(DPrimWorld<float>);
+        out->world_prims = f.world_ok ? f.wprims.size() : 0;
         return NRT_OK;
     });
 }
@@ -485,7 +490,7 @@ int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, co
             device_zero(ctr, 8 * sizeof(uint64_t), dev);
             p.out = (float*)img;
             p.counters = (unsigned long long*)ctr;
-            gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, nullptr);
+            gpu_launch_render(ds, p, opts ? opts->precision : 0, opts ? opts->rng : 0, opts ? opts->trace : 0, nullptr);
             device_sync(dev);
             uint64_t h[8];
             device_copy_to_host(h, ctr, sizeof h, dev);

@@ -73,6 +73,27 @@ struct alignas(16) DPrimFast {
     uint32_t pad[2];
 };
 
+// Fast kernel, world-space mode (instances flattened away; MAXD = 0 kernels).
+// A quad/triangle reached through a Translate/Rotate/Scale chain whose
+// world->object map is o' = M o + b keeps the reference's object-space
+// arithmetic when its planes are pulled back to world space: n.o' = d becomes
+// (M^T n).o = d - n.b, alpha = A.o' - a0 becomes (M^T A).o - (a0 - A.b), and
+// t is the same in both spaces (directions are transformed, not normalised).
+// The front-face sign of the reference, signum(d'.n), is signum(d.(M^T n)); the
+// shading normal is the object normal mapped out by the chain's rotations only
+// (Q11: Scale leaves normals alone).  Spheres qualify under translations only.
+template <typename Real>
+struct alignas(16) DPrimWorld {
+    Real N[3];      // plane: M^T n (unnormalised)   sphere: world center at time 0
+    Real D;         // plane: d - n.b                sphere: radius
+    Real A[3];      // plane: M^T (v x w)            sphere: speed
+    Real a0;        // plane: a0 - A.b
+    Real B[3];      // plane: M^T (w x u)
+    Real b0;        // plane: b0 - B.b
+    Real S[3];      // plane: shading normal (rotations of the chain applied to n)
+    uint32_t meta;  // kind | material << 2
+};
+
 template <typename Real>
 struct alignas(16) DXform {
     // TRANSLATE: m[0..2] = offset
@@ -144,6 +165,8 @@ struct DSceneView {
     const DInstFast<Real>* inst_fast;  // fast kernel: composed instance transforms
     const DMatFast* mats_fast;         // fast kernel: materials with inline solid colour
     uint32_t n_fprims, n_inst_fast, n_mats_fast;
+    const DPrimWorld<Real>* wprims;  // fast kernel, world-space mode (MAXD = 0); not LDS-staged
+    uint32_t n_wprims;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each

@@ -183,7 +183,7 @@ struct Flattener {
         inst.first_xform = (uint32_t)out.xforms.size();
         const Object* t = o;
         while (is_transform(t)) {
-            xform(t);
+            xform_of[t] = xform(t);
             t = t->child.get();
         }
         inst.num_xforms = (uint32_t)out.xforms.size() - inst.first_xform;
@@ -345,6 +345,99 @@ struct Flattener {
         return end > begin ? (int32_t)begin : NODE_END;
     }
 
+    // ---- world-space primitives (fast kernel, MAXD = 0 mode; device_scene.hpp DPrimWorld)
+    static constexpr size_t WORLD_PRIM_CAP = size_t(1) << 22;
+    using M3a = std::array<double, 9>;  // column major
+    using V3a = std::array<double, 3>;
+    struct Affine {
+        M3a M{1, 0, 0, 0, 1, 0, 0, 0, 1};  // world -> object: o' = M o + b
+        V3a b{0, 0, 0};
+        M3a R{1, 0, 0, 0, 1, 0, 0, 0, 1};  // object normal -> world (rotations only)
+        bool translate_only = true;
+    };
+    static M3a mmul(const M3a& a, const M3a& c) {
+        M3a r{};
+        for (int col = 0; col < 3; ++col)
+            for (int row = 0; row < 3; ++row)
+                r[3 * col + row] = a[row] * c[3 * col] + a[3 + row] * c[3 * col + 1] + a[6 + row] * c[3 * col + 2];
+        return r;
+    }
+    static V3a mvec(const M3a& a, const V3a& v) {
+        return {a[0] * v[0] + a[3] * v[1] + a[6] * v[2], a[1] * v[0] + a[4] * v[1] + a[7] * v[2],
+                a[2] * v[0] + a[5] * v[1] + a[8] * v[2]};
+    }
+    static V3a mtvec(const M3a& a, const V3a& v) {  // a^T v
+        return {a[0] * v[0] + a[1] * v[1] + a[2] * v[2], a[3] * v[0] + a[4] * v[1] + a[5] * v[2],
+                a[6] * v[0] + a[7] * v[1] + a[8] * v[2]};
+    }
+    static V3a va(V3 v) { return {v.x, v.y, v.z}; }
+    static double vdot(const V3a& a, const V3a& c) { return a[0] * c[0] + a[1] * c[1] + a[2] * c[2]; }
+
+    void world_walk(const Object* o, const Affine& f) {
+        if (!out.world_ok) return;
+        switch (o->kind) {
+            case Object::BvhEmpty: return;
+            case Object::BvhLeaf: world_walk(o->child.get(), f); return;
+            case Object::BvhNode: world_walk(o->left.get(), f); world_walk(o->right.get(), f); return;
+            case Object::Sphere: {
+                if (!f.translate_only) { out.world_ok = false; return; }  // uv needs the object frame
+                DPrimWorld<double> w{};
+                const V3a c = va(o->center);
+                for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.A[k] = va(o->speed)[k]; }
+                w.D = o->radius;
+                w.meta = PRIM_SPHERE | (material(o->material) << 2);
+                out.wprims.push_back(w);
+                break;
+            }
+            case Object::Quad:
+            case Object::Triangle: {
+                const V3a n = va(o->normal), Aq = va(cross(o->v, o->w)), Bq = va(cross(o->w, o->u));
+                const double a0 = dot(o->p, cross(o->v, o->w)), b0 = dot(o->p, cross(o->w, o->u));
+                const V3a N = mtvec(f.M, n), A = mtvec(f.M, Aq), B = mtvec(f.M, Bq), S = mvec(f.R, n);
+                DPrimWorld<double> w{};
+                for (int k = 0; k < 3; ++k) { w.N[k] = N[k]; w.A[k] = A[k]; w.B[k] = B[k]; w.S[k] = S[k]; }
+                w.D = o->d - vdot(n, f.b);
+                w.a0 = a0 - vdot(Aq, f.b);
+                w.b0 = b0 - vdot(Bq, f.b);
+                w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (material(o->material) << 2);
+                out.wprims.push_back(w);
+                break;
+            }
+            case Object::Translate: {
+                Affine g = f;
+                for (int k = 0; k < 3; ++k) g.b[k] -= va(o->offset)[k];
+                world_walk(o->child.get(), g);
+                return;
+            }
+            case Object::Rotate:
+            case Object::Scale: {
+                const DXform<double>& x = out.xforms[xform_index(o)];
+                M3a L, Linv;
+                for (int q = 0; q < 9; ++q) { L[q] = x.m[q]; Linv[q] = x.inv[q]; }
+                Affine g;
+                g.M = mmul(L, f.M);
+                g.b = mvec(L, f.b);
+                g.R = f.R;
+                g.translate_only = false;
+                if (o->kind == Object::Scale) {
+                    for (int k = 0; k < 3; ++k) g.b[k] += x.m[9 + k];
+                } else {
+                    g.R = mmul(f.R, Linv);
+                }
+                world_walk(o->child.get(), g);
+                return;
+            }
+        }
+        if (out.wprims.size() > WORLD_PRIM_CAP) out.world_ok = false;
+    }
+    // DXform of a transform node (every chain was emitted by instance()).
+    std::map<const Object*, uint32_t> xform_of;
+    uint32_t xform_index(const Object* t) {
+        auto it = xform_of.find(t);
+        if (it == xform_of.end()) throw std::runtime_error("internal: transform without an instance");
+        return it->second;
+    }
+
     int32_t tree(const Object* o) {
         const uint32_t begin = (uint32_t)out.nodes.size();
         emit(o);
@@ -411,6 +504,9 @@ struct Flattener {
             throw std::runtime_error("instance nesting depth " + std::to_string(out.max_depth) + " exceeds " +
                                      std::to_string(MAX_INSTANCE_DEPTH));
         out.num_trees = (uint32_t)tree_ranges.size();
+        out.world_ok = true;
+        world_walk(top, Affine{});
+        if (!out.world_ok) out.wprims.clear();
     }
 };
 
@@ -451,6 +547,16 @@ FlatScene32 to_f32(const FlatScene& s) {
         for (int k = 0; k < 3; ++k) { b.n[k] = (float)a.n[k]; b.A[k] = (float)a.A[k]; b.B[k] = (float)a.B[k]; }
         b.d = (float)a.d; b.a0 = (float)a.a0; b.b0 = (float)a.b0;
         b.kind = a.kind; b.material = a.material; b.pad[0] = b.pad[1] = 0;
+    }
+    o.wprims.resize(s.wprims.size());
+    for (size_t i = 0; i < s.wprims.size(); ++i) {
+        const auto& a = s.wprims[i];
+        auto& b = o.wprims[i];
+        for (int k = 0; k < 3; ++k) {
+            b.N[k] = (float)a.N[k]; b.A[k] = (float)a.A[k]; b.B[k] = (float)a.B[k]; b.S[k] = (float)a.S[k];
+        }
+        b.D = (float)a.D; b.a0 = (float)a.a0; b.b0 = (float)a.b0;
+        b.meta = a.meta;
     }
     o.inst_fast.resize(s.inst_fast.size());
     for (size_t i = 0; i < s.inst_fast.size(); ++i) {

@@ -25,6 +25,10 @@ struct FlatScene {
     int32_t root = NODE_END;
     int32_t max_depth = 0;
     uint32_t num_trees = 0;
+    // World-space primitives in the reference's depth-first candidate order
+    // (device_scene.hpp DPrimWorld); world_ok = every primitive qualifies.
+    std::vector<DPrimWorld<double>> wprims;
+    bool world_ok = false;
 };
 
 FlatScene flatten_scene(const ObjectPtr& top_level_bvh);
@@ -37,6 +41,7 @@ struct FlatScene32 {
     std::vector<DXform<float>> xforms;
     std::vector<DInstFast<float>> inst_fast;
     std::vector<DPrimFast<float>> fprims;
+    std::vector<DPrimWorld<float>> wprims;
 };
 FlatScene32 to_f32(const FlatScene& s);
 

@@ -12,7 +12,9 @@
 //   Real  = float  : the fast variant (reciprocal slab test, f32 RNG floats)
 //   RNG   = ChaCha8 per-pixel stream (rand_chacha 0.9, bit-exact with the
 //           reference) or Philox4x32-10 keyed per (pixel, sample, draw)
-//   MAXD  = 1 when instances do not nest (all BASELINE scenes), 4 otherwise.
+//   MAXD  = 1 when instances do not nest (all BASELINE scenes), 4 otherwise;
+//           0 = world-space mode (fast kernel only): instances flattened away
+//           on the host, every lane tests every primitive (small scenes).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -463,8 +465,68 @@ struct HitMin {
     R t;
     uint32_t prim;
     int depth;
-    uint32_t inst[MAXD];
+    uint32_t inst[MAXD > 0 ? MAXD : 1];
 };
+
+// World-space mode (MAXD = 0, fast kernel): the wave tests every primitive in
+// the reference's depth-first candidate order (`t <= t_best`: the later
+// candidate wins ties, as in trace).  The primitive index is wave-uniform, so
+// each record is read once per wave through the scalar cache into SGPRs (the
+// constant address space makes the loads s_load), and no lane diverges.
+template <typename R>
+using ConstPrimWorld = const __attribute__((address_space(4))) DPrimWorld<R>*;
+template <typename R>
+__device__ __forceinline__ DPrimWorld<R> load_world(ConstPrimWorld<R> p) {
+    DPrimWorld<R> q;
+    for (int c = 0; c < 3; ++c) { q.N[c] = p->N[c]; q.A[c] = p->A[c]; q.B[c] = p->B[c]; q.S[c] = p->S[c]; }
+    q.D = p->D;
+    q.a0 = p->a0;
+    q.b0 = p->b0;
+    q.meta = p->meta;
+    return q;
+}
+
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
+    const ConstPrimWorld<R> wp = (ConstPrimWorld<R>)sc.wprims;
+    R t_best = R(INFINITY);
+    int32_t best = -1;
+    const uint32_t n = sc.n_wprims;  // >= 1 (host picks this mode only for non-empty lists)
+    DPrimWorld<R> next = load_world(wp);
+    for (uint32_t k = 0; k < n; ++k) {
+        const DPrimWorld<R> q = next;
+        if (k + 1 < n) next = load_world(wp + k + 1);  // scalar prefetch: overlaps the s_load with this test
+        const uint32_t kind = q.meta & 3u;
+        R t;
+        bool ok;
+        if (kind == PRIM_SPHERE) {
+            DPrim<R> sp;
+            for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.A[c]; }
+            sp.s = q.D;
+            t = sphere_t(sp, ray);
+            ok = t >= R(0) && t <= t_best;
+        } else {
+            const V<R> nrm = ld3(q.N);
+            const R denom = dot(nrm, ray.d);
+            t = (q.D - dot(nrm, ray.o)) * fast_rcp(denom);
+            const V<R> pt = ray.o + t * ray.d;
+            const R alpha = dot(pt, ld3(q.A)) - q.a0;
+            const R beta = dot(pt, ld3(q.B)) - q.b0;
+            bool inside;  // comparisons, not min/max: a NaN coordinate never hits
+            if (kind == PRIM_QUAD)  // closed [0, 1]^2 (plane.rs:121-126)
+                inside = (alpha >= R(0)) & (alpha <= R(1)) & (beta >= R(0)) & (beta <= R(1));
+            else  // open triangle (plane.rs:128-133)
+                inside = (alpha > R(0)) & (beta > R(0)) & (alpha + beta < R(1));
+            ok = (fabs(denom) >= R(1e-8)) & (t >= R(0.001)) & (t <= t_best) & inside;
+        }
+        t_best = ok ? t : t_best;
+        best = ok ? (int32_t)k : best;
+    }
+    hm.t = t_best;
+    hm.prim = (uint32_t)best;
+    hm.depth = 0;
+    return best >= 0;
+}
 
 // Closest hit over the flattened scene ("while-while": lanes first run through
 // inner nodes until each holds a leaf, then leaves are processed together).
@@ -473,7 +535,7 @@ struct HitMin {
 // `if l.t < r.t {l} else {r}` (object.rs:109-115).  Only (t, prim, instance
 // path) is kept; the winner's record is rebuilt afterwards (make_record).
 template <typename R, int MAXD, bool EXACT>
-__device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
     R t_best = R(INFINITY);
     bool found = false;
     int32_t node = sc.root;
@@ -571,10 +633,48 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
     return found;
 }
 
-// HitRecord of the winner, recomputed exactly as the candidate test computed it
+template <typename R, int MAXD, bool EXACT>
+__device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    if constexpr (MAXD == 0) return trace_world(sc, wray, hm);
+    else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm);
+}
+
+// HitRecord of the winner (HitRecord::new_with_uv, hitable.rs:38-59).
+// World-space record (MAXD = 0; device_scene.hpp DPrimWorld): the
+// reference's front-face sign signum(d'.n) = signum(d.(M^T n)), shading normal
+// mapped out by the chain's rotations only.
+template <typename R, int MAXD>
+__device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
+                                                     const HitMin<R, MAXD>& hm) {
+    const DPrimWorld<R> q = sc.wprims[hm.prim];
+    Rec<R> h;
+    h.p = wray.o + hm.t * wray.d;
+    V<R> geo, shade;
+    if ((q.meta & 3u) == PRIM_SPHERE) {
+        const V<R> center = ld3(q.N) + wray.time * ld3(q.A);
+        geo = normalize(h.p - center);
+        shade = geo;
+        const R theta = acos(-geo.y);
+        const R phi = atan2(-geo.z, geo.x) + R(M_PI);
+        h.u = phi * R(1.0 / (2.0 * M_PI));
+        h.v = theta * R(1.0 / M_PI);
+    } else {
+        h.u = dot(h.p, ld3(q.A)) - q.a0;
+        h.v = dot(h.p, ld3(q.B)) - q.b0;
+        geo = ld3(q.N);
+        shade = ld3(q.S);
+    }
+    const R sign = signum(dot(wray.d, geo));
+    h.front = sign < R(0);
+    h.n = (-sign) * shade;
+    h.mat = q.meta >> 2;
+    return h;
+}
+
+// Instance mode: recomputed exactly as the candidate test computed it
 // (object-space point / normal / uv, then mapped out through the instances).
 template <typename R, int MAXD, bool EXACT>
-__device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
     Ray<R> ray = wray;
     auto enter = [&](uint32_t iid) {
         if constexpr (EXACT) xform_in<R, true>(sc, sc.instances[iid], ray);
@@ -637,6 +737,12 @@ __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray
         for (int l = hm.depth - 1; l >= 0; --l) leave(hm.inst[l], h);
     }
     return h;
+}
+
+template <typename R, int MAXD, bool EXACT>
+__device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
+    if constexpr (MAXD == 0) return make_record_world(sc, wray, hm);
+    else return make_record_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
 // ----------------------------------------------------------------- shading

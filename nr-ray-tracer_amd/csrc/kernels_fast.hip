@@ -6,14 +6,16 @@
 
 namespace nrt {
 
-void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, bool deep, hipStream_t stream) {
-    if (rng == RNG_CHACHA8) {
-        if (deep) launch_one<float, dev::ChaCha8, MAX_INSTANCE_DEPTH, false>(p, v, stream);
-        else launch_one<float, dev::ChaCha8, 1, false>(p, v, stream);
-    } else {
-        if (deep) launch_one<float, dev::Philox, MAX_INSTANCE_DEPTH, false>(p, v, stream);
-        else launch_one<float, dev::Philox, 1, false>(p, v, stream);
-    }
+template <class G>
+static void launch_fast_rng(const RenderParams& p, const DSceneView<float>& v, int maxd, hipStream_t stream) {
+    if (maxd == 0) launch_one<float, G, 0, false>(p, v, stream);
+    else if (maxd == 1) launch_one<float, G, 1, false>(p, v, stream);
+    else launch_one<float, G, MAX_INSTANCE_DEPTH, false>(p, v, stream);
+}
+
+void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, int maxd, hipStream_t stream) {
+    if (rng == RNG_CHACHA8) launch_fast_rng<dev::ChaCha8>(p, v, maxd, stream);
+    else launch_fast_rng<dev::Philox>(p, v, maxd, stream);
 }
 
 }  // namespace nrt

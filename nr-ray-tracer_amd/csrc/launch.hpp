@@ -12,8 +12,10 @@
 
 namespace nrt {
 
-void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, bool deep, hipStream_t stream);
-void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, bool deep, hipStream_t stream);
+// maxd: instance nesting the kernel supports (1 or MAX_INSTANCE_DEPTH); the
+// fast kernel also takes 0 = world-space mode (DSceneView::wprims).
+void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, int maxd, hipStream_t stream);
+void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, int maxd, hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
                       unsigned long long* d_out);
 

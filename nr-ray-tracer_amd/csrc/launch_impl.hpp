@@ -17,9 +17,13 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_
     const uint32_t ring = G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0;
     const uint32_t scene = lds_scene_bytes(v);
     if (p.counters) {  // diagnostic phase profile (nrt_debug_phase_profile)
-        if (scene > LDS_SCENE_LIMIT || MAXD != 1) throw std::runtime_error("phase profile: LDS-resident, flat-instance scenes only");
-        hipLaunchKernelGGL((dev::render_kernel<R, G, 1, EXACT, true, true>), dim3(blocks), dim3(dev::BLOCK),
-                           ring + scene, stream, p, v);
+        if constexpr (MAXD > 1) {
+            throw std::runtime_error("phase profile: LDS-resident, flat-instance scenes only");
+        } else {
+            if (scene > LDS_SCENE_LIMIT) throw std::runtime_error("phase profile: LDS-resident scenes only");
+            hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true, true>), dim3(blocks), dim3(dev::BLOCK),
+                               ring + scene, stream, p, v);
+        }
     } else if (scene <= LDS_SCENE_LIMIT) {
         hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true>), dim3(blocks), dim3(dev::BLOCK), ring + scene,
                            stream, p, v);

@@ -11,6 +11,7 @@
 
 #include "flatten.hpp"
 #include "gpu.hpp"
+#include "nrt.h"
 
 // =====================================================================
 // Host side: device buffers and launches (no torch types, plain HIP).
@@ -40,6 +41,7 @@ struct DeviceScene {
     DSceneView<float> v32{};
     std::vector<void*> allocations;
     size_t bytes = 0;
+    bool world_ok = false;  // fast kernel may run in world-space mode (v32.wprims)
 };
 
 int gpu_device_count() {
@@ -69,18 +71,21 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* ifast = (DInstFast<float>*)track(upload(f32.inst_fast, "inst_fast"),
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
         auto* mfast = (DMatFast*)track(upload(fs.mats_fast, "mats_fast"), fs.mats_fast.size() * sizeof(DMatFast));
+        auto* wpr = (DPrimWorld<float>*)track(upload(f32.wprims, "wprims"), f32.wprims.size() * sizeof(DPrimWorld<float>));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
                        ni = (uint32_t)fs.instances.size(), nm = (uint32_t)fs.materials.size(),
                        nt = (uint32_t)fs.textures.size();
         // f64 view: the exact node array (reference node for node); f32 view: the
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
-                                     (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0};
+                                     (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
+                                     nullptr, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
-                                    (uint32_t)fs.mats_fast.size()};
+                                    (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size()};
+        ds->world_ok = fs.world_ok;
     } catch (...) {
         gpu_free_scene(ds);
         throw;
@@ -101,14 +106,27 @@ void gpu_free_scene(DeviceScene* ds) {
 size_t gpu_scene_bytes(const DeviceScene* ds) { return ds ? ds->bytes : 0; }
 int gpu_scene_device(const DeviceScene* ds) { return ds ? ds->device : -1; }
 
+// Fast kernel traversal mode for `trace` (nrt_render_opts.trace): world-space
+// list when every primitive could be pulled to world space and the list is
+// short enough that testing all of it beats per-lane BVH traversal.
+int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace) {
+    const int inst_maxd = ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1;
+    if (trace == NRT_TRACE_BVH) return inst_maxd;
+    const bool world = ds->world_ok && ds->v32.n_wprims > 0;
+    if (trace == NRT_TRACE_WORLD_LIST) {
+        if (!world) throw std::invalid_argument("trace=world-list: scene has primitives that cannot be flattened to world space");
+        return 0;
+    }
+    return (world && ds->v32.n_wprims <= NRT_WORLD_LIST_MAX) ? 0 : inst_maxd;
+}
+
 void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng,
-                       void* stream_ptr) {
+                       uint32_t trace, void* stream_ptr) {
     if (p.pixel_end <= p.pixel_begin) return;
     if (p.width == 0) throw std::runtime_error("width must be > 0");
     hipStream_t stream = (hipStream_t)stream_ptr;
-    const bool deep = ds->v64.max_depth > 1;
-    if (precision == 0) launch_exact(p, ds->v64, rng, deep, stream);
-    else launch_fast(p, ds->v32, rng, deep, stream);
+    if (precision == 0) launch_exact(p, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, stream);
+    else launch_fast(p, ds->v32, rng, gpu_fast_maxd(ds, trace), stream);
     check(hipGetLastError(), "render kernel launch");
 }
 

@@ -24,6 +24,7 @@ LIB_PATH = os.path.join(_HERE, "libnrt.so")
 
 PRECISION = {"f64": 0, "f32": 1}
 RNG = {"chacha8": 0, "philox": 1}
+TRACE = {"auto": 0, "bvh": 1, "world-list": 2}  # nrt_trace (f32 kernel traversal)
 
 NRT_OK = 0
 ERRORS = {-1: "invalid argument", -2: "load error", -3: "device error", -4: "unsupported"}
@@ -60,13 +61,13 @@ class _Camera(C.Structure):
 
 class _RenderOpts(C.Structure):
     _fields_ = [("precision", C.c_uint32), ("rng", C.c_uint32), ("device", C.c_int32), ("row_offset", C.c_uint32),
-                ("row_stride", C.c_uint32), ("reserved", C.c_uint32 * 3)]
+                ("row_stride", C.c_uint32), ("trace", C.c_uint32), ("reserved", C.c_uint32 * 2)]
 
 
 class _SceneStats(C.Structure):
     _fields_ = [("nodes", C.c_uint64), ("prims", C.c_uint64), ("instances", C.c_uint64), ("xforms", C.c_uint64),
                 ("materials", C.c_uint64), ("textures", C.c_uint64), ("texels", C.c_uint64), ("trees", C.c_uint32),
-                ("max_instance_depth", C.c_uint32), ("device_bytes", C.c_uint64)]
+                ("max_instance_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("world_prims", C.c_uint64)]
 
 
 PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
@@ -279,14 +280,17 @@ class CameraBuilder:
         return Camera._from_c(out)
 
 
-def _opts(precision: str, rng: str, device: int, row_offset: int, row_stride: int) -> _RenderOpts:
+def _opts(precision: str, rng: str, device: int, row_offset: int, row_stride: int,
+          trace: str = "auto") -> _RenderOpts:
     if precision not in PRECISION:
         raise ValueError(f"precision must be one of {list(PRECISION)}")
     if rng not in RNG:
         raise ValueError(f"rng must be one of {list(RNG)}")
+    if trace not in TRACE:
+        raise ValueError(f"trace must be one of {list(TRACE)}")
     o = _RenderOpts()
     o.precision, o.rng, o.device = PRECISION[precision], RNG[rng], device
-    o.row_offset, o.row_stride = row_offset, row_stride
+    o.row_offset, o.row_stride, o.trace = row_offset, row_stride, TRACE[trace]
     return o
 
 
@@ -336,12 +340,12 @@ class Scene:
 
     def render(self, camera: Optional[Camera] = None, precision: str = "f64", rng: str = "chacha8",
                device: int = -1, row_offset: int = 0, row_stride: int = 1,
-               progress: Optional[Callable[[int], None]] = None) -> np.ndarray:
+               progress: Optional[Callable[[int], None]] = None, trace: str = "auto") -> np.ndarray:
         """Camera::render -> Rgb32FImage as float32 array (rows, W, 3)."""
         cam = camera or self.camera
         if cam is None:
             raise ValueError("no camera")
-        o = _opts(precision, rng, device, row_offset, row_stride)
+        o = _opts(precision, rng, device, row_offset, row_stride, trace)
         rows = lib().nrt_rows_selected(cam.height, C.byref(o))
         out = np.empty((rows, cam.width, 3), dtype=np.float32)
         cb = PROGRESS_FN(lambda _u, n: progress(n)) if progress else PROGRESS_FN()
@@ -350,10 +354,10 @@ class Scene:
         return out
 
     def phase_profile(self, camera: Optional[Camera] = None, precision: str = "f32", rng: str = "philox",
-                      device: int = -1) -> dict:
+                      device: int = -1, trace: str = "auto") -> dict:
         """Diagnostic render with per-wave stamps: cycle shares of camera / trace / shading."""
         cam = camera or self.camera
-        o = _opts(precision, rng, device, 0, 1)
+        o = _opts(precision, rng, device, 0, 1, trace)
         out = (C.c_uint64 * 5)()
         _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 5))
         iters, cam_c, trace_c, shade_c, waves = list(out)
@@ -364,10 +368,10 @@ class Scene:
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",
                       rng: str = "philox", device: int = -1, row_offset: int = 0, row_stride: int = 1,
-                      stream: int = 0) -> None:
+                      stream: int = 0, trace: str = "auto") -> None:
         """Enqueue a render into device memory (e.g. a torch tensor's data_ptr) on a HIP stream."""
         cam = camera or self.camera
-        o = _opts(precision, rng, device, row_offset, row_stride)
+        o = _opts(precision, rng, device, row_offset, row_stride, trace)
         _check(lib().nrt_render_device(self._h, C.byref(cam._c()), C.byref(o), C.c_void_p(out_ptr), out_len,
                                        C.c_void_p(stream)))
 

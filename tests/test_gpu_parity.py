@@ -95,9 +95,10 @@ STAT_CASES = [("scenes/cornell-box-scene.json", 48, 48, 64), ("scenes/spheres.to
               ("scenes/cube-scene.json", 40, 30, 32)]
 
 
-@pytest.mark.parametrize("precision,rng", [("f32", "chacha8"), ("f32", "philox"), ("f64", "philox")])
+@pytest.mark.parametrize("precision,rng,trace", [("f32", "chacha8", "auto"), ("f32", "philox", "auto"),
+                                                 ("f64", "philox", "auto"), ("f32", "philox", "bvh")])
 @pytest.mark.parametrize("case", STAT_CASES, ids=[c[0] for c in STAT_CASES])
-def test_fast_variants_statistically_match(precision, rng, case):
+def test_fast_variants_statistically_match(precision, rng, trace, case):
     """Statistical parity: image means within 4.5 standard errors,
     per-pixel z-scores (std from the oracle's per-sample variance) with mean
     z^2 in [0.5, 2] and < 1 % of pixels beyond |z| > 6."""
@@ -108,7 +109,7 @@ def test_fast_variants_statistically_match(precision, rng, case):
     want = want.astype(np.float64)
     var = np.maximum(var.astype(np.float64), 0.0)
     s = load(scene, w, h, spp)
-    got = s.render(precision=precision, rng=rng).reshape(-1).astype(np.float64)
+    got = s.render(precision=precision, rng=rng, trace=trace).reshape(-1).astype(np.float64)
     assert np.all(np.isfinite(got))
     # both images are means of spp samples: Var(got - want) ~ 2 var / spp for independent streams
     se_pix = np.sqrt(2.0 * var / spp)
@@ -161,13 +162,16 @@ def test_empty_and_degenerate_inputs():
 
 @pytest.mark.parametrize("scene,w,h", [(c[0], c[1], c[2]) for c in CASES_F64[:5]])
 @pytest.mark.parametrize("bounces", [1, 2, 3])
-def test_fast_kernel_follows_exact_paths(scene, w, h, bounces):
-    """The f32 kernel (leaf lists, composed instance transforms) must follow the
-    same paths as the exact kernel on the same ChaCha8 stream: with few bounces
-    any geometry bug shows as whole faces of mismatching pixels, while genuine
-    f32 rounding flips stay rare."""
+@pytest.mark.parametrize("trace", ["bvh", "world-list"])
+def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
+    """The f32 kernel (leaf lists + composed instance transforms, or the
+    world-space list) must follow the same paths as the exact kernel on the
+    same ChaCha8 stream: with few bounces any geometry bug shows as whole faces
+    of mismatching pixels, while genuine f32 rounding flips stay rare."""
     s = load(scene, w, h, 1, bounces)
-    a = s.render(precision="f32", rng="chacha8")
+    if trace == "world-list" and s.stats()["world_prims"] == 0:
+        pytest.skip("scene does not flatten to world space")
+    a = s.render(precision="f32", rng="chacha8", trace=trace)
     b = s.render(precision="f64", rng="chacha8")
     mismatch = np.mean(np.abs(a - b).max(axis=2) > 1e-3 + 1e-3 * np.abs(b).max(axis=2))
     assert mismatch <= 0.01, mismatch
