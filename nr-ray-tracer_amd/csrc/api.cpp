@@ -170,6 +170,10 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         p.defocus_disk_u[k] = c.defocus_disk_u[k];
         p.defocus_disk_v[k] = c.defocus_disk_v[k];
         p.background[k] = c.background_color[k];
+        const double* vs[7] = {c.top_left, c.pixel_delta_u, c.pixel_delta_v, c.look_from, c.defocus_disk_u,
+                               c.defocus_disk_v, c.background_color};
+        for (int q = 0; q < 7; ++q) p.camf[q][k] = (float)vs[q][k];
+        if (c.defocus_disk_u[k] != 0.0 || c.defocus_disk_v[k] != 0.0) p.defocus = 1;
     }
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;

@@ -137,6 +137,7 @@ __device__ __forceinline__ void chacha8_block(uint32_t ctr_lo, uint32_t ctr_hi, 
 // block per 8-9 draw steps even when lanes have drifted apart.
 struct ChaCha8 {
     static constexpr bool uses_lds = true;
+    static constexpr bool exact_stream = true;  // draws must follow the reference's sequence
     uint32_t s_lo, s_hi, ctr, head, count;
     uint2* ring;  // slot k of this lane at ring[k * BLOCK]
 
@@ -188,6 +189,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 
 struct Philox {
     static constexpr bool uses_lds = false;
+    static constexpr bool exact_stream = false;  // only the distributions matter
     uint32_t pix, sample, pair;
     uint32_t w0, w1, w2, w3;  // unread words of the current block, consumed in order
     uint32_t left;
@@ -274,7 +276,40 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_di
     }
 }
 
-// ----------------------------------------------------------------- geometry
+// Philox mode: the same distributions as the two rejection samplers, drawn
+// directly (no data-dependent loop, so no lane waits for another's retries).
+// p uniform in the unit ball, p/|p|^2 = u/r with u uniform on the sphere and
+// r = U^(1/3); p uniform in the unit disk, p/|p|^2 = (cos t, sin t)/sqrt(U).
+template <typename R, class G> __device__ __forceinline__ V<R> unit_ball_inverse(G& g) {
+    const R z = draw<R>(g, R(-1), R(1));
+    const R turn = draw<R>(g, R(0), R(1));
+    const R w = R(1) - draw<R>(g, R(0), R(1));  // (0, 1]
+    const R s = sqrt(fmax(R(0), R(1) - z * z));
+    if constexpr (sizeof(R) == 4) {
+        const float inv_r = __builtin_amdgcn_exp2f(-0.333333343f * __builtin_amdgcn_logf(w));
+        const float c = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn);  // argument in turns
+        return (inv_r * s) * mk(c, sn, R(0)) + mk(R(0), R(0), inv_r * z);
+    } else {
+        double sn, c;
+        sincospi(2.0 * turn, &sn, &c);
+        const double inv_r = 1.0 / cbrt(w);
+        return mk(inv_r * s * c, inv_r * s * sn, inv_r * z);
+    }
+}
+template <typename R, class G> __device__ __forceinline__ V<R> unit_disk_inverse(G& g) {
+    const R turn = draw<R>(g, R(0), R(1));
+    const R w = R(1) - draw<R>(g, R(0), R(1));  // (0, 1]
+    if constexpr (sizeof(R) == 4) {
+        const float inv_r = __builtin_amdgcn_rsqf(w);
+        return mk(inv_r * __builtin_amdgcn_cosf(turn), inv_r * __builtin_amdgcn_sinf(turn), 0.0f);
+    } else {
+        double sn, c;
+        sincospi(2.0 * turn, &sn, &c);
+        const double inv_r = 1.0 / sqrt(w);
+        return mk(inv_r * c, inv_r * sn, 0.0);
+    }
+}
+
 // ----------------------------------------------------------------- geometry
 template <typename R>
 struct Ray {
@@ -853,10 +888,13 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
     G g;
     g.init(n, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);
 
-    const V<R> top_left = ld3d<R>(p.top_left), du = ld3d<R>(p.pixel_delta_u), dv = ld3d<R>(p.pixel_delta_v);
-    const V<R> look_from = ld3d<R>(p.look_from), disk_u = ld3d<R>(p.defocus_disk_u),
-               disk_v = ld3d<R>(p.defocus_disk_v);
-    const V<R> background = ld3d<R>(p.background);
+    auto cam = [&](int q, const double* d) {  // f32 kernel: host-rounded copies stay in SGPRs
+        if constexpr (sizeof(R) == 4) return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
+        else return ld3d<R>(d);
+    };
+    const V<R> top_left = cam(0, p.top_left), du = cam(1, p.pixel_delta_u), dv = cam(2, p.pixel_delta_v);
+    const V<R> look_from = cam(3, p.look_from), disk_u = cam(4, p.defocus_disk_u), disk_v = cam(5, p.defocus_disk_v);
+    const V<R> background = cam(6, p.background);
 
     double ax = 0.0, ay = 0.0, az = 0.0;
     uint32_t s = 0, b = 0;
@@ -876,8 +914,12 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
                 oy = draw<R>(g, R(-0.5), R(0.5));
             }
             const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
-            const V<R> disk = random_in_unit_disk<R>(g);
-            ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+            if (G::exact_stream || p.defocus) {
+                const V<R> disk = G::exact_stream ? random_in_unit_disk<R>(g) : unit_disk_inverse<R>(g);
+                ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+            } else {
+                ray.o = look_from;  // zero disk: the draws would only scale zero vectors
+            }
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
             prep_ray<R, EXACT>(ray);
@@ -933,7 +975,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
                         if (!refl) refl = reflectance(cos_theta, ri) > draw<R>(g, R(0.0), R(1.0));
                         dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
                     } else {
-                        const V<R> rs = random_in_unit_sphere<R>(g);
+                        const V<R> rs = G::exact_stream ? random_in_unit_sphere<R>(g) : unit_ball_inverse<R>(g);
                         if (mkind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
                             dir = h.n + rs;
                             if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;

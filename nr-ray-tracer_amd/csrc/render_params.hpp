@@ -16,6 +16,11 @@ struct RenderParams {
     double defocus_disk_u[3];
     double defocus_disk_v[3];
     double background[3];
+    // The same seven vectors rounded to f32 (in this order: top_left, delta_u,
+    // delta_v, look_from, disk_u, disk_v, background) for the f32 kernel, so
+    // they stay in SGPRs instead of being converted per lane.
+    float camf[7][3];
+    uint32_t defocus;  // 0: defocus disk is zero (defocus_angle <= 0), disk draws only feed the origin
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;
