@@ -86,13 +86,15 @@ template <typename Real>
 struct alignas(16) DPrimWorld {
     Real N[3];      // plane: M^T n (unnormalised)   sphere: world center at time 0
     Real D;         // plane: d - n.b                sphere: radius
-    Real A[3];      // plane: M^T (v x w)            sphere: speed
-    Real a0;        // plane: a0 - A.b
-    Real B[3];      // plane: M^T (w x u)
-    Real b0;        // plane: b0 - B.b
+    // plane: (A.x, B.x, A.y, B.y, A.z, B.z, a0', b0') with A = M^T (v x w),
+    // B = M^T (w x u), a0' = a0 - (v x w).b, b0' = b0 - (w x u).b: pairs, so the
+    // kernel gets (alpha, beta) from packed FMAs;   sphere: speed in [0..2]
+    Real AB[8];
     Real S[3];      // plane: shading normal (rotations of the chain applied to n)
     uint32_t meta;  // kind | material << 2
 };
+// Consecutive primitives of one kind form a run (kind | count << 2), so the
+// kernel's inner loops are kind-specialised without reordering candidates.
 
 template <typename Real>
 struct alignas(16) DXform {
@@ -167,6 +169,8 @@ struct DSceneView {
     uint32_t n_fprims, n_inst_fast, n_mats_fast;
     const DPrimWorld<Real>* wprims;  // fast kernel, world-space mode (MAXD = 0); not LDS-staged
     uint32_t n_wprims;
+    const uint32_t* wruns;           // runs of same-kind world primitives
+    uint32_t n_wruns;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each

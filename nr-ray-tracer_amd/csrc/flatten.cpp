@@ -383,7 +383,7 @@ struct Flattener {
                 if (!f.translate_only) { out.world_ok = false; return; }  // uv needs the object frame
                 DPrimWorld<double> w{};
                 const V3a c = va(o->center);
-                for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.A[k] = va(o->speed)[k]; }
+                for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.AB[k] = va(o->speed)[k]; }
                 w.D = o->radius;
                 w.meta = PRIM_SPHERE | (material(o->material) << 2);
                 out.wprims.push_back(w);
@@ -395,10 +395,10 @@ struct Flattener {
                 const double a0 = dot(o->p, cross(o->v, o->w)), b0 = dot(o->p, cross(o->w, o->u));
                 const V3a N = mtvec(f.M, n), A = mtvec(f.M, Aq), B = mtvec(f.M, Bq), S = mvec(f.R, n);
                 DPrimWorld<double> w{};
-                for (int k = 0; k < 3; ++k) { w.N[k] = N[k]; w.A[k] = A[k]; w.B[k] = B[k]; w.S[k] = S[k]; }
+                for (int k = 0; k < 3; ++k) { w.N[k] = N[k]; w.AB[2 * k] = A[k]; w.AB[2 * k + 1] = B[k]; w.S[k] = S[k]; }
                 w.D = o->d - vdot(n, f.b);
-                w.a0 = a0 - vdot(Aq, f.b);
-                w.b0 = b0 - vdot(Bq, f.b);
+                w.AB[6] = a0 - vdot(Aq, f.b);
+                w.AB[7] = b0 - vdot(Bq, f.b);
                 w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (material(o->material) << 2);
                 out.wprims.push_back(w);
                 break;
@@ -507,6 +507,13 @@ struct Flattener {
         out.world_ok = true;
         world_walk(top, Affine{});
         if (!out.world_ok) out.wprims.clear();
+        for (const auto& w : out.wprims) {
+            const uint32_t kind = w.meta & 3u;
+            if (!out.wruns.empty() && (out.wruns.back() & 3u) == kind && (out.wruns.back() >> 2) < (1u << 29))
+                out.wruns.back() += 4u;
+            else
+                out.wruns.push_back(kind | 4u);
+        }
     }
 };
 
@@ -552,10 +559,9 @@ FlatScene32 to_f32(const FlatScene& s) {
     for (size_t i = 0; i < s.wprims.size(); ++i) {
         const auto& a = s.wprims[i];
         auto& b = o.wprims[i];
-        for (int k = 0; k < 3; ++k) {
-            b.N[k] = (float)a.N[k]; b.A[k] = (float)a.A[k]; b.B[k] = (float)a.B[k]; b.S[k] = (float)a.S[k];
-        }
-        b.D = (float)a.D; b.a0 = (float)a.a0; b.b0 = (float)a.b0;
+        for (int k = 0; k < 3; ++k) { b.N[k] = (float)a.N[k]; b.S[k] = (float)a.S[k]; }
+        for (int k = 0; k < 8; ++k) b.AB[k] = (float)a.AB[k];
+        b.D = (float)a.D;
         b.meta = a.meta;
     }
     o.inst_fast.resize(s.inst_fast.size());

@@ -28,6 +28,7 @@ struct FlatScene {
     // World-space primitives in the reference's depth-first candidate order
     // (device_scene.hpp DPrimWorld); world_ok = every primitive qualifies.
     std::vector<DPrimWorld<double>> wprims;
+    std::vector<uint32_t> wruns;  // kind | count << 2 over wprims
     bool world_ok = false;
 };
 

@@ -510,52 +510,50 @@ struct HitMin {
 // constant address space makes the loads s_load), and no lane diverges.
 template <typename R>
 using ConstPrimWorld = const __attribute__((address_space(4))) DPrimWorld<R>*;
-template <typename R>
-__device__ __forceinline__ DPrimWorld<R> load_world(ConstPrimWorld<R> p) {
-    DPrimWorld<R> q;
-    for (int c = 0; c < 3; ++c) { q.N[c] = p->N[c]; q.A[c] = p->A[c]; q.B[c] = p->B[c]; q.S[c] = p->S[c]; }
-    q.D = p->D;
-    q.a0 = p->a0;
-    q.b0 = p->b0;
-    q.meta = p->meta;
-    return q;
-}
+using ConstU32 = const __attribute__((address_space(4))) uint32_t*;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename R, int MAXD>
 __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
-    const ConstPrimWorld<R> wp = (ConstPrimWorld<R>)sc.wprims;
-    R t_best = R(INFINITY);
+    static_assert(sizeof(R) == 4, "world-space mode is an f32-kernel mode");
+    const ConstPrimWorld<float> wp = (ConstPrimWorld<float>)sc.wprims;
+    const ConstU32 runs = (ConstU32)sc.wruns;
+    float t_best = INFINITY;
     int32_t best = -1;
-    const uint32_t n = sc.n_wprims;  // >= 1 (host picks this mode only for non-empty lists)
-    DPrimWorld<R> next = load_world(wp);
-    for (uint32_t k = 0; k < n; ++k) {
-        const DPrimWorld<R> q = next;
-        if (k + 1 < n) next = load_world(wp + k + 1);  // scalar prefetch: overlaps the s_load with this test
-        const uint32_t kind = q.meta & 3u;
-        R t;
-        bool ok;
+    // (d, o) pairs: N.d and N.o come out of one packed FMA chain
+    const f32x2 dox = {ray.d.x, ray.o.x}, doy = {ray.d.y, ray.o.y}, doz = {ray.d.z, ray.o.z};
+    uint32_t k = 0;
+    for (uint32_t r = 0; r < sc.n_wruns; ++r) {
+        const uint32_t run = runs[r];
+        const uint32_t kind = run & 3u, end = k + (run >> 2);
         if (kind == PRIM_SPHERE) {
-            DPrim<R> sp;
-            for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.A[c]; }
-            sp.s = q.D;
-            t = sphere_t(sp, ray);
-            ok = t >= R(0) && t <= t_best;
-        } else {
-            const V<R> nrm = ld3(q.N);
-            const R denom = dot(nrm, ray.d);
-            t = (q.D - dot(nrm, ray.o)) * fast_rcp(denom);
-            const V<R> pt = ray.o + t * ray.d;
-            const R alpha = dot(pt, ld3(q.A)) - q.a0;
-            const R beta = dot(pt, ld3(q.B)) - q.b0;
-            bool inside;  // comparisons, not min/max: a NaN coordinate never hits
-            if (kind == PRIM_QUAD)  // closed [0, 1]^2 (plane.rs:121-126)
-                inside = (alpha >= R(0)) & (alpha <= R(1)) & (beta >= R(0)) & (beta <= R(1));
-            else  // open triangle (plane.rs:128-133)
-                inside = (alpha > R(0)) & (beta > R(0)) & (alpha + beta < R(1));
-            ok = (fabs(denom) >= R(1e-8)) & (t >= R(0.001)) & (t <= t_best) & inside;
+            for (; k < end; ++k) {
+                DPrim<R> sp;
+                for (int c = 0; c < 3; ++c) { sp.a[c] = wp[k].N[c]; sp.b[c] = wp[k].AB[c]; }
+                sp.s = wp[k].D;
+                const float t = sphere_t(sp, ray);
+                const bool ok = (t >= 0.0f) & (t <= t_best);
+                t_best = ok ? t : t_best;
+                best = ok ? (int32_t)k : best;
+            }
+            continue;
         }
-        t_best = ok ? t : t_best;
-        best = ok ? (int32_t)k : best;
+        const bool quad = kind == PRIM_QUAD;
+        for (; k < end; ++k) {
+            const ConstPrimWorld<float> q = wp + k;
+            const f32x2 dn = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];  // (N.d, N.o)
+            const float t = (q->D - dn.y) * __builtin_amdgcn_rcpf(dn.x);
+            const float px = ray.o.x + t * ray.d.x, py = ray.o.y + t * ray.d.y, pz = ray.o.z + t * ray.d.z;
+            const f32x2 ab = f32x2{q->AB[0], q->AB[1]} * px + f32x2{q->AB[2], q->AB[3]} * py +
+                             f32x2{q->AB[4], q->AB[5]} * pz - f32x2{q->AB[6], q->AB[7]};  // (alpha, beta)
+            const float lo = fminf(ab.x, ab.y);
+            // quad closed [0,1]^2 (plane.rs:121-126), triangle open (plane.rs:128-133); a NaN
+            // coordinate can only come from a rejected denominator or t
+            const bool inside = quad ? (lo >= 0.0f) & (ab.x <= 1.0f) & (ab.y <= 1.0f) : (lo > 0.0f) & (ab.x + ab.y < 1.0f);
+            const bool ok = (fabsf(dn.x) >= 1e-8f) & (t >= 0.001f) & (t <= t_best) & inside;
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)k : best;
+        }
     }
     hm.t = t_best;
     hm.prim = (uint32_t)best;
@@ -686,7 +684,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     h.p = wray.o + hm.t * wray.d;
     V<R> geo, shade;
     if ((q.meta & 3u) == PRIM_SPHERE) {
-        const V<R> center = ld3(q.N) + wray.time * ld3(q.A);
+        const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
         geo = normalize(h.p - center);
         shade = geo;
         const R theta = acos(-geo.y);
@@ -694,8 +692,8 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
         h.u = phi * R(1.0 / (2.0 * M_PI));
         h.v = theta * R(1.0 / M_PI);
     } else {
-        h.u = dot(h.p, ld3(q.A)) - q.a0;
-        h.v = dot(h.p, ld3(q.B)) - q.b0;
+        h.u = dot(h.p, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
+        h.v = dot(h.p, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
         geo = ld3(q.N);
         shade = ld3(q.S);
     }

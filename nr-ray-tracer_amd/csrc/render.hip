@@ -72,6 +72,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
         auto* mfast = (DMatFast*)track(upload(fs.mats_fast, "mats_fast"), fs.mats_fast.size() * sizeof(DMatFast));
         auto* wpr = (DPrimWorld<float>*)track(upload(f32.wprims, "wprims"), f32.wprims.size() * sizeof(DPrimWorld<float>));
+        auto* wrn = (uint32_t*)track(upload(fs.wruns, "wruns"), fs.wruns.size() * sizeof(uint32_t));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
                        ni = (uint32_t)fs.instances.size(), nm = (uint32_t)fs.materials.size(),
                        nt = (uint32_t)fs.textures.size();
@@ -79,12 +80,13 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0};
+                                     nullptr, 0, nullptr, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
-                                    (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size()};
+                                    (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
+                                    (uint32_t)fs.wruns.size()};
         ds->world_ok = fs.world_ok;
     } catch (...) {
         gpu_free_scene(ds);
