@@ -36,7 +36,7 @@ enum nrt_precision { NRT_PRECISION_F64 = 0, NRT_PRECISION_F32 = 1 };
 enum nrt_rng { NRT_RNG_CHACHA8 = 0, NRT_RNG_PHILOX = 1 };
 /* Traversal of the f32 kernel (the f64 kernel always walks the reference's BVH):
  * AUTO picks WORLD_LIST for scenes whose primitives all flatten to world space
- * and number at most NRT_WORLD_LIST_MAX, else BVH (instances kept, per-lane
+ * and make at most NRT_WORLD_LIST_MAX test units (nrt_scene_stats.world_prims), else BVH (instances kept, per-lane
  * traversal).  WORLD_LIST fails with NRT_E_INVALID on scenes that cannot flatten. */
 enum nrt_trace { NRT_TRACE_AUTO = 0, NRT_TRACE_BVH = 1, NRT_TRACE_WORLD_LIST = 2 };
 #define NRT_WORLD_LIST_MAX 48
@@ -121,7 +121,8 @@ typedef struct {
     uint64_t nodes, prims, instances, xforms, materials, textures, texels;
     uint32_t trees, max_instance_depth;
     uint64_t device_bytes; /* HBM bytes of the flattened scene on one device */
-    uint64_t world_prims;  /* primitives after flattening instances to world space (0: not flattenable) */
+    uint64_t world_prims;  /* world-list test units after flattening instances to world space: primitives,
+                              with six quads closing a box counted once (0: not flattenable) */
 } nrt_scene_stats;
 
 typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);

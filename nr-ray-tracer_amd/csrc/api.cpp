@@ -445,7 +445,7 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
                             f.nodes_fast.size() * sizeof(DNode<float>) + f.fprims.size() * sizeof(DPrimFast<float>) +
                             f.inst_fast.size() * sizeof(DInstFast<float>) + f.mats_fast.size() * sizeof(DMatFast) +
                             f.wprims.size() * sizeof(DPrimWorld<float>);
-        out->world_prims = f.world_ok ? f.wprims.size() : 0;
+        out->world_prims = f.world_ok ? f.world_units : 0;
         return NRT_OK;
     });
 }

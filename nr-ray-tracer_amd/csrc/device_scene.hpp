@@ -29,7 +29,7 @@ enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2, NODE_LIST = 
 // primitive in the subtree's depth-first order, stored contiguously in the fast
 // primitive array.  meta = 3 | (count-1) << 2 | first << 8.
 constexpr uint32_t LIST_MAX = 8;
-enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2 };
+enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2, PRIM_BOX = 3 /* world mode only */ };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2 };
@@ -93,8 +93,17 @@ struct alignas(16) DPrimWorld {
     Real S[3];      // plane: shading normal (rotations of the chain applied to n)
     uint32_t meta;  // kind | material << 2
 };
-// Consecutive primitives of one kind form a run (kind | count << 2), so the
-// kernel's inner loops are kind-specialised without reordering candidates.
+// PRIM_BOX (world mode): six consecutive quads that close a parallelepiped
+// {c + a e1 + b e2 + g e3 : a, b, g in [0, 1]} are tested as one slab test in
+// its local frame x' = E^-1 x - E^-1 c.  The header entry holds the rows of
+// E^-1 and E^-1 c as (N, D), (AB[0..2], AB[3]), (AB[4..6], AB[7]); meta =
+// PRIM_BOX | face << 2 with 3 bits per (axis, side) naming which of the six
+// quads that follow the header lies on plane x'_axis = side.  The quads keep
+// their own records (uv, normals, material) for the hit record.
+constexpr uint32_t BOX_ENTRIES = 7;
+// Consecutive units of one kind form a run (kind | count << 2; a box unit is
+// BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised
+// without reordering candidates.
 
 template <typename Real>
 struct alignas(16) DXform {

@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <array>
 #include <deque>
 #include <map>
@@ -371,6 +372,112 @@ struct Flattener {
                 a[6] * v[0] + a[7] * v[1] + a[8] * v[2]};
     }
     static V3a va(V3 v) { return {v.x, v.y, v.z}; }
+    static M3a inverse3(const M3a& m) {  // column major; adjugate / determinant
+        const double a = m[0], b = m[3], c = m[6], d = m[1], e = m[4], f = m[7], g = m[2], h = m[5], i = m[8];
+        const double A = e * i - f * h, B = -(d * i - f * g), C = d * h - e * g;
+        const double det = a * A + b * B + c * C;
+        const double r = 1.0 / det;
+        M3a o;  // o[3*col + row]
+        o[0] = A * r; o[3] = -(b * i - c * h) * r; o[6] = (b * f - c * e) * r;
+        o[1] = B * r; o[4] = (a * i - c * g) * r; o[7] = -(a * f - c * d) * r;
+        o[2] = C * r; o[5] = -(a * h - b * g) * r; o[8] = (a * e - b * d) * r;
+        return o;
+    }
+    std::vector<std::array<V3a, 3>> wgeom;  // world (p, u, v) of each world prim (quads; zero otherwise)
+
+    // Six consecutive quads closing a parallelepiped -> PRIM_BOX header (device_scene.hpp).
+    bool fuse_box(size_t i, DPrimWorld<double>& hdr) const {
+        std::vector<V3a> pts;
+        double scale = 0;
+        for (size_t q = i; q < i + 6; ++q) {
+            if ((out.wprims[q].meta & 3u) != PRIM_QUAD) return false;
+            const auto& g = wgeom[q];
+            const V3a c[4] = {g[0], {g[0][0] + g[1][0], g[0][1] + g[1][1], g[0][2] + g[1][2]},
+                              {g[0][0] + g[2][0], g[0][1] + g[2][1], g[0][2] + g[2][2]},
+                              {g[0][0] + g[1][0] + g[2][0], g[0][1] + g[1][1] + g[2][1], g[0][2] + g[1][2] + g[2][2]}};
+            for (const V3a& x : c) {
+                pts.push_back(x);
+                for (int k = 0; k < 3; ++k) scale = std::max(scale, std::fabs(x[k]));
+            }
+        }
+        const double tol = 1e-9 * std::max(scale, 1e-300);
+        auto same = [&](const V3a& a, const V3a& b) {
+            return std::fabs(a[0] - b[0]) <= tol && std::fabs(a[1] - b[1]) <= tol && std::fabs(a[2] - b[2]) <= tol;
+        };
+        std::vector<V3a> uniq;
+        std::vector<int> mult;
+        for (const V3a& x : pts) {
+            size_t k = 0;
+            while (k < uniq.size() && !same(uniq[k], x)) ++k;
+            if (k == uniq.size()) { uniq.push_back(x); mult.push_back(0); }
+            ++mult[k];
+        }
+        if (uniq.size() != 8) return false;
+        for (int m : mult) if (m != 3) return false;
+        auto has = [&](const V3a& x) {
+            for (const V3a& u : uniq) if (same(u, x)) return true;
+            return false;
+        };
+        const auto& g0 = wgeom[i];
+        const V3a c = g0[0], e1 = g0[1], e2 = g0[2];
+        V3a e3{};
+        bool found = false;
+        for (const V3a& r : uniq) {
+            const V3a w{r[0] - c[0], r[1] - c[1], r[2] - c[2]};
+            if (std::fabs(w[0]) <= tol && std::fabs(w[1]) <= tol && std::fabs(w[2]) <= tol) continue;
+            auto plus = [&](const V3a& a, const V3a& b) { return V3a{a[0] + b[0], a[1] + b[1], a[2] + b[2]}; };
+            if (has(plus(c, w)) && has(plus(plus(c, e1), w)) && has(plus(plus(c, e2), w)) &&
+                has(plus(plus(plus(c, e1), e2), w)) && !same(plus(c, w), plus(c, e1)) && !same(plus(c, w), plus(c, e2)) &&
+                !same(plus(c, w), plus(plus(c, e1), e2))) {
+                e3 = w;
+                found = true;
+                break;
+            }
+        }
+        if (!found) return false;
+        const M3a E{e1[0], e1[1], e1[2], e2[0], e2[1], e2[2], e3[0], e3[1], e3[2]};
+        const double det = E[0] * (E[4] * E[8] - E[7] * E[5]) - E[3] * (E[1] * E[8] - E[7] * E[2]) +
+                           E[6] * (E[1] * E[5] - E[4] * E[2]);
+        const double vol = std::sqrt(vdot(e1, e1) * vdot(e2, e2) * vdot(e3, e3));
+        if (!(std::fabs(det) > 1e-9 * vol)) return false;
+        const M3a Ei = inverse3(E);
+        const V3a cl = mvec(Ei, c);
+        int face[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};
+        for (size_t q = 0; q < 6; ++q) {
+            const auto& g = wgeom[i + q];
+            int onaxis = -1, side = -1, combos = 0;
+            for (int a = 0; a < 3; ++a) {
+                int vals = 0;  // bit0: some corner at 0, bit1: some corner at 1
+                for (int k = 0; k < 4; ++k) {
+                    V3a x = g[0];
+                    for (int r = 0; r < 3; ++r) x[r] += ((k & 1) ? g[1][r] : 0.0) + ((k & 2) ? g[2][r] : 0.0);
+                    const V3a l = mvec(Ei, x);
+                    const double la = l[a] - cl[a];
+                    if (std::fabs(la) <= 1e-6) vals |= 1;
+                    else if (std::fabs(la - 1.0) <= 1e-6) vals |= 2;
+                    else return false;
+                }
+                if (vals == 3) ++combos;
+                else { onaxis = a; side = vals == 1 ? 0 : 1; }
+            }
+            if (onaxis < 0 || combos != 2 || face[onaxis][side] >= 0) return false;
+            face[onaxis][side] = (int)q;
+        }
+        hdr = DPrimWorld<double>{};
+        for (int k = 0; k < 3; ++k) {  // rows of E^-1 (column-major Ei[3*col + row])
+            hdr.N[k] = Ei[3 * k + 0];
+            hdr.AB[k] = Ei[3 * k + 1];
+            hdr.AB[4 + k] = Ei[3 * k + 2];
+        }
+        hdr.D = cl[0];
+        hdr.AB[3] = cl[1];
+        hdr.AB[7] = cl[2];
+        uint32_t map = 0;
+        for (int a = 0; a < 3; ++a)
+            for (int sd = 0; sd < 2; ++sd) map |= (uint32_t)face[a][sd] << (3 * (2 * a + sd));
+        hdr.meta = PRIM_BOX | (map << 2);
+        return true;
+    }
     static double vdot(const V3a& a, const V3a& c) { return a[0] * c[0] + a[1] * c[1] + a[2] * c[2]; }
 
     void world_walk(const Object* o, const Affine& f) {
@@ -387,6 +494,7 @@ struct Flattener {
                 w.D = o->radius;
                 w.meta = PRIM_SPHERE | (material(o->material) << 2);
                 out.wprims.push_back(w);
+                wgeom.push_back({});
                 break;
             }
             case Object::Quad:
@@ -394,6 +502,12 @@ struct Flattener {
                 const V3a n = va(o->normal), Aq = va(cross(o->v, o->w)), Bq = va(cross(o->w, o->u));
                 const double a0 = dot(o->p, cross(o->v, o->w)), b0 = dot(o->p, cross(o->w, o->u));
                 const V3a N = mtvec(f.M, n), A = mtvec(f.M, Aq), B = mtvec(f.M, Bq), S = mvec(f.R, n);
+                {  // world-space parallelogram (for box fusion): x = M^-1 (x' - b)
+                    const M3a Mi = inverse3(f.M);
+                    const V3a p0 = va(o->p);
+                    wgeom.push_back({mvec(Mi, {p0[0] - f.b[0], p0[1] - f.b[1], p0[2] - f.b[2]}), mvec(Mi, va(o->u)),
+                                     mvec(Mi, va(o->v))});
+                }
                 DPrimWorld<double> w{};
                 for (int k = 0; k < 3; ++k) { w.N[k] = N[k]; w.AB[2 * k] = A[k]; w.AB[2 * k + 1] = B[k]; w.S[k] = S[k]; }
                 w.D = o->d - vdot(n, f.b);
@@ -507,8 +621,25 @@ struct Flattener {
         out.world_ok = true;
         world_walk(top, Affine{});
         if (!out.world_ok) out.wprims.clear();
-        for (const auto& w : out.wprims) {
-            const uint32_t kind = w.meta & 3u;
+        // fuse closed boxes, then group units into same-kind runs (order kept)
+        std::vector<DPrimWorld<double>> fused;
+        std::vector<uint32_t> kinds;
+        for (size_t i = 0; i < out.wprims.size();) {
+            DPrimWorld<double> hdr;
+            if (i + 6 <= out.wprims.size() && fuse_box(i, hdr)) {
+                fused.push_back(hdr);
+                fused.insert(fused.end(), out.wprims.begin() + i, out.wprims.begin() + i + 6);
+                kinds.push_back(PRIM_BOX);
+                i += 6;
+            } else {
+                fused.push_back(out.wprims[i]);
+                kinds.push_back(out.wprims[i].meta & 3u);
+                ++i;
+            }
+        }
+        out.wprims.swap(fused);
+        out.world_units = kinds.size();
+        for (uint32_t kind : kinds) {
             if (!out.wruns.empty() && (out.wruns.back() & 3u) == kind && (out.wruns.back() >> 2) < (1u << 29))
                 out.wruns.back() += 4u;
             else

@@ -29,6 +29,7 @@ struct FlatScene {
     // (device_scene.hpp DPrimWorld); world_ok = every primitive qualifies.
     std::vector<DPrimWorld<double>> wprims;
     std::vector<uint32_t> wruns;  // kind | count << 2 over wprims
+    uint64_t world_units = 0;     // primitives + fused boxes: the world list's test count
     bool world_ok = false;
 };
 

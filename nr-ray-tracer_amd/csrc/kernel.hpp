@@ -528,6 +528,27 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     for (uint32_t r = 0; r < sc.n_wruns; ++r) {
         const uint32_t run = runs[r];
         const uint32_t kind = run & 3u, end = k + (run >> 2);
+        if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
+            for (uint32_t b = 0; b < (run >> 2); ++b, k += BOX_ENTRIES) {
+                const ConstPrimWorld<float> q = wp + k;
+                // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
+                const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
+                const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
+                const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
+                const float ix = __builtin_amdgcn_rcpf(lx.x), iy = __builtin_amdgcn_rcpf(ly.x),
+                            iz = __builtin_amdgcn_rcpf(lz.x);
+                const float ax = (q->D - lx.y) * ix, ay = (q->AB[3] - ly.y) * iy, az = (q->AB[7] - lz.y) * iz;
+                const float bx = ax + ix, by = ay + iy, bz = az + iz;  // planes x' = 0 and x' = 1
+                const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                // entry face unless it lies before t_min (origin on or inside the box): then the exit face
+                const float t = tn >= 0.001f ? tn : tf;
+                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+                t_best = ok ? t : t_best;
+                best = ok ? (int32_t)k : best;
+            }
+            continue;
+        }
         if (kind == PRIM_SPHERE) {
             for (; k < end; ++k) {
                 DPrim<R> sp;
@@ -681,7 +702,23 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
 template <typename R, int MAXD>
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
-    const DPrimWorld<R> q = sc.wprims[hm.prim];
+    uint32_t prim = hm.prim;
+    if ((sc.wprims[prim].meta & 3u) == PRIM_BOX) {
+        // which face: the local coordinate of the hit point nearest a face plane
+        const DPrimWorld<R> b = sc.wprims[prim];
+        const V<R> pw = wray.o + hm.t * wray.d;
+        const R l[3] = {dot(ld3(b.N), pw) - b.D, dot(ld3(b.AB), pw) - b.AB[3], dot(ld3(b.AB + 4), pw) - b.AB[7]};
+        uint32_t slot = 0;
+        R dmin = R(INFINITY);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const R d0 = fabs(l[a]), d1 = fabs(l[a] - R(1));
+            if (d0 < dmin) { dmin = d0; slot = 2 * a; }
+            if (d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
+        }
+        prim += 1 + ((b.meta >> (2 + 3 * slot)) & 7u);
+    }
+    const DPrimWorld<R> q = sc.wprims[prim];
     Rec<R> h;
     h.p = wray.o + hm.t * wray.d;
     V<R> geo, shade;

@@ -42,6 +42,7 @@ struct DeviceScene {
     std::vector<void*> allocations;
     size_t bytes = 0;
     bool world_ok = false;  // fast kernel may run in world-space mode (v32.wprims)
+    uint64_t world_units = 0;
 };
 
 int gpu_device_count() {
@@ -88,6 +89,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
                                     (uint32_t)fs.wruns.size()};
         ds->world_ok = fs.world_ok;
+        ds->world_units = fs.world_units;
     } catch (...) {
         gpu_free_scene(ds);
         throw;
@@ -119,7 +121,7 @@ int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace) {
         if (!world) throw std::invalid_argument("trace=world-list: scene has primitives that cannot be flattened to world space");
         return 0;
     }
-    return (world && ds->v32.n_wprims <= NRT_WORLD_LIST_MAX) ? 0 : inst_maxd;
+    return (world && ds->world_units <= NRT_WORLD_LIST_MAX) ? 0 : inst_maxd;
 }
 
 void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng,
