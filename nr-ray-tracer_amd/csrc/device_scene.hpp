@@ -176,7 +176,7 @@ struct DSceneView {
     const DInstFast<Real>* inst_fast;  // fast kernel: composed instance transforms
     const DMatFast* mats_fast;         // fast kernel: materials with inline solid colour
     uint32_t n_fprims, n_inst_fast, n_mats_fast;
-    const DPrimWorld<Real>* wprims;  // fast kernel, world-space mode (MAXD = 0); not LDS-staged
+    const DPrimWorld<Real>* wprims;  // fast kernel, world-space mode (MAXD = 0)
     uint32_t n_wprims;
     const uint32_t* wruns;           // runs of same-kind world primitives
     uint32_t n_wruns;
@@ -192,7 +192,7 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
            r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>)) +
-           r16(v.n_mats_fast * sizeof(DMatFast));
+           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * sizeof(DPrimWorld<Real>));
 }
 
 }  // namespace nrt

@@ -885,6 +885,7 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.fprims = (const DPrimFast<R>*)copy(g.fprims, g.n_fprims * (uint32_t)sizeof(DPrimFast<R>));
     s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
     s.mats_fast = (const DMatFast*)copy(g.mats_fast, g.n_mats_fast * (uint32_t)sizeof(DMatFast));
+    s.wprims = (const DPrimWorld<R>*)copy(g.wprims, g.n_wprims * (uint32_t)sizeof(DPrimWorld<R>));
     __syncthreads();
     return s;
 }
@@ -972,7 +973,8 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
         V<R> contrib = mk(R(0), R(0), R(0));
         if (b < p.max_bounces) {  // depth cap returns black (Q6)
             HitMin<R, MAXD> hm;
-            const bool hit = trace<R, MAXD, EXACT>(sc, ray, hm);
+            // world mode tests the list through the scalar cache (global view); records read LDS
+            const bool hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm);
             t2 = stamp();
             if (!hit) {
                 contrib = tp * background;

@@ -24,7 +24,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_
             hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true, true>), dim3(blocks), dim3(dev::BLOCK),
                                ring + scene, stream, p, v);
         }
-    } else if (scene <= LDS_SCENE_LIMIT && MAXD != 0) {  // world mode reads prims via the scalar cache
+    } else if (scene <= LDS_SCENE_LIMIT) {
         hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true>), dim3(blocks), dim3(dev::BLOCK), ring + scene,
                            stream, p, v);
     } else {

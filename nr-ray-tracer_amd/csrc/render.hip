@@ -130,7 +130,16 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     if (p.width == 0) throw std::runtime_error("width must be > 0");
     hipStream_t stream = (hipStream_t)stream_ptr;
     if (precision == 0) launch_exact(p, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, stream);
-    else launch_fast(p, ds->v32, rng, gpu_fast_maxd(ds, trace), stream);
+    else {
+        const int maxd = gpu_fast_maxd(ds, trace);
+        DSceneView<float> v = ds->v32;  // stage (LDS) only the tables this mode reads
+        if (maxd == 0) {
+            v.n_nodes = v.n_fprims = v.n_inst_fast = v.n_instances = 0;
+        } else {
+            v.n_wprims = 0;
+        }
+        launch_fast(p, v, rng, maxd, stream);
+    }
     check(hipGetLastError(), "render kernel launch");
 }
 
