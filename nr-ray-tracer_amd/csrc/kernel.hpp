@@ -223,7 +223,20 @@ struct Philox {
         const uint32_t lo = next32();
         return (uint64_t)lo | ((uint64_t)next32() << 32);
     }
+    // Render loop: one whole block per lane per iteration, counter
+    // (pixel, sample, step): step 0 = camera ray, b + 1 = scatter at bounce b.
+    __device__ __forceinline__ uint4 block(uint32_t smp, uint32_t step) const {
+        uint32_t w[4];
+        philox4x32_10(pix, smp, step, 0u, 0u, 0u, w);
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    }
 };
+constexpr uint32_t PHILOX_STEP_DEFOCUS = 0xFFFFFFFFu;  // second camera block when the defocus disk is on
+
+// 32-bit word -> uniform [0, 1) (f32: 23 bits, f64: 32 bits)
+template <typename R> __device__ __forceinline__ R u01(uint32_t w);
+template <> __device__ __forceinline__ float u01<float>(uint32_t w) { return __uint_as_float(0x3F800000u | (w >> 9)) - 1.0f; }
+template <> __device__ __forceinline__ double u01<double>(uint32_t w) { return (double)w * 0x1p-32; }
 
 // rand 0.9 `random_range(low..high)` / `(low..=high)` on f64: one draw,
 // value1_2 = from_bits((u >> 12) | 1.0.to_bits()), (value1_2 - 1) * scale + low.
@@ -282,10 +295,10 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_di
 // directly (no data-dependent loop, so no lane waits for another's retries).
 // p uniform in the unit ball, p/|p|^2 = u/r with u uniform on the sphere and
 // r = U^(1/3); p uniform in the unit disk, p/|p|^2 = (cos t, sin t)/sqrt(U).
-template <typename R, class G> __device__ __forceinline__ V<R> unit_ball_inverse(G& g) {
-    const R z = draw<R>(g, R(-1), R(1));
-    const R turn = draw<R>(g, R(0), R(1));
-    const R w = R(1) - draw<R>(g, R(0), R(1));  // (0, 1]
+template <typename R> __device__ __forceinline__ V<R> unit_ball_inverse(uint32_t w0, uint32_t w1, uint32_t w2) {
+    const R z = R(2) * u01<R>(w0) - R(1);
+    const R turn = u01<R>(w1);
+    const R w = R(1) - u01<R>(w2);  // (0, 1]
     const R s = sqrt(fmax(R(0), R(1) - z * z));
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_exp2f(-0.333333343f * __builtin_amdgcn_logf(w));
@@ -298,9 +311,9 @@ template <typename R, class G> __device__ __forceinline__ V<R> unit_ball_inverse
         return mk(inv_r * s * c, inv_r * s * sn, inv_r * z);
     }
 }
-template <typename R, class G> __device__ __forceinline__ V<R> unit_disk_inverse(G& g) {
-    const R turn = draw<R>(g, R(0), R(1));
-    const R w = R(1) - draw<R>(g, R(0), R(1));  // (0, 1]
+template <typename R> __device__ __forceinline__ V<R> unit_disk_inverse(uint32_t w0, uint32_t w1) {
+    const R turn = u01<R>(w0);
+    const R w = R(1) - u01<R>(w1);  // (0, 1]
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_rsqf(w);
         return mk(inv_r * __builtin_amdgcn_cosf(turn), inv_r * __builtin_amdgcn_sinf(turn), 0.0f);
@@ -935,31 +948,48 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
     const V<R> background = cam(6, p.background);
 
     double ax = 0.0, ay = 0.0, az = 0.0;
-    uint32_t s = 0, b = 0;
+    uint32_t s = 0, b = 0, cur = 0;  // samples started, bounces of this path, current sample
     bool fresh = true, bounced = false;
     Ray<R> ray;
     V<R> tp = mk(R(1), R(1), R(1));
+    // Philox mode: the block this lane consumes next (exactly one per loop
+    // iteration, computed by every lane at the same point: no divergent refills)
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (!G::exact_stream) w = g.block(0u, 0u);
     while (true) {
         const unsigned long long t0 = stamp();
         if (fresh) {
             if (s >= p.spp) break;
             g.start_sample(s);
-            ++s;
+            cur = s++;
             // Camera::get_ray (camera.rs:244-267)
             R ox = R(0), oy = R(0);
-            if (p.spp > 1) {
-                ox = draw<R>(g, R(-0.5), R(0.5));
-                oy = draw<R>(g, R(-0.5), R(0.5));
+            if constexpr (G::exact_stream) {
+                if (p.spp > 1) {
+                    ox = draw<R>(g, R(-0.5), R(0.5));
+                    oy = draw<R>(g, R(-0.5), R(0.5));
+                }
+            } else if (p.spp > 1) {
+                ox = u01<R>(w.x) - R(0.5);
+                oy = u01<R>(w.y) - R(0.5);
             }
             const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
-            if (G::exact_stream || p.defocus) {
-                const V<R> disk = G::exact_stream ? random_in_unit_disk<R>(g) : unit_disk_inverse<R>(g);
+            if constexpr (G::exact_stream) {
+                const V<R> disk = random_in_unit_disk<R>(g);
                 ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+                ray.d = point - ray.o;
+                ray.time = draw<R>(g, R(0.0), R(1.0));
             } else {
-                ray.o = look_from;  // zero disk: the draws would only scale zero vectors
+                if (p.defocus) {
+                    const uint4 wd = g.block(cur, PHILOX_STEP_DEFOCUS);
+                    const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
+                    ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+                } else {
+                    ray.o = look_from;  // zero disk: the draws would only scale zero vectors
+                }
+                ray.d = point - ray.o;
+                ray.time = u01<R>(w.z);
             }
-            ray.d = point - ray.o;
-            ray.time = draw<R>(g, R(0.0), R(1.0));
             prep_ray<R, EXACT>(ray);
             tp = mk(R(1), R(1), R(1));
             b = 0;
@@ -969,8 +999,14 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
         const unsigned long long t1 = stamp();
         unsigned long long t2 = t1;
         // one step of get_ray_color (camera.rs:269-300): L = a0*(a1*(...*T))
-        bool term = true;
+        bool term = true, scatter = false;
         V<R> contrib = mk(R(0), R(0), R(0));
+        Rec<R> h;
+        uint32_t mkind = 0, mtex = 0;
+        R mparam = R(0);
+        bool msolid = false;
+        V<R> mcolor = mk(R(0), R(0), R(0));
+        auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
         if (b < p.max_bounces) {  // depth cap returns black (Q6)
             HitMin<R, MAXD> hm;
             // world mode tests the list through the scalar cache (global view); records read LDS
@@ -979,11 +1015,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
             if (!hit) {
                 contrib = tp * background;
             } else {
-                const Rec<R> h = make_record<R, MAXD, EXACT>(sc, ray, hm);
-                uint32_t mkind, mtex;
-                R mparam;
-                bool msolid = false;
-                V<R> mcolor;
+                h = make_record<R, MAXD, EXACT>(sc, ray, hm);
                 if constexpr (EXACT) {
                     const DMaterial m = sc.materials[h.mat];
                     mkind = m.kind;
@@ -997,43 +1029,57 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, con
                     msolid = m.solid != 0;
                     mcolor = mk(m.color[0], m.color[1], m.color[2]);
                 }
-                auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
                 if (mkind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
                     const R k = bounced ? mparam : R(1.0);
                     contrib = tp * (k * albedo());
                 } else {
-                    V<R> dir;
-                    V<R> att = mk(R(1), R(1), R(1));
-                    bool scattered = true;
-                    if (mkind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
-                        const R ri = h.front ? R(1.0) / mparam : mparam;
-                        const V<R> unit = normalize(ray.d);
-                        const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
-                        const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
-                        bool refl = ri * sin_theta > R(1.0);
-                        if (!refl) refl = reflectance(cos_theta, ri) > draw<R>(g, R(0.0), R(1.0));
-                        dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
-                    } else {
-                        const V<R> rs = G::exact_stream ? random_in_unit_sphere<R>(g) : unit_ball_inverse<R>(g);
-                        if (mkind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
-                            dir = h.n + rs;
-                            if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
-                        } else {  // metal.rs:73-91 (draws even when fuzz = 0, Q5)
-                            dir = normalize(reflect(ray.d, h.n)) + mparam * rs;
-                            scattered = dot(dir, h.n) > R(0.0);  // else absorbed: emitted = 0
-                        }
-                        if (scattered) att = albedo();
-                    }
-                    if (scattered) {
-                        tp = tp * att;
-                        ray.o = h.p;
-                        ray.d = dir;
-                        prep_ray<R, EXACT>(ray);
-                        bounced = true;
-                        ++b;
-                        term = false;
-                    }
+                    scatter = true;
                 }
+            }
+        }
+        // Philox: this iteration's block -- the scatter's (pixel, sample, bounce + 1), or, when
+        // the path ends here, the next sample's camera block (pixel, sample + 1, 0)
+        if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + 1, scatter ? b + 1 : 0u);
+        if (scatter) {
+            V<R> dir;
+            V<R> att = mk(R(1), R(1), R(1));
+            bool scattered = true;
+            if (mkind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
+                const R ri = h.front ? R(1.0) / mparam : mparam;
+                const V<R> unit = normalize(ray.d);
+                const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
+                const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
+                bool refl = ri * sin_theta > R(1.0);
+                if (!refl) {
+                    R r;
+                    if constexpr (G::exact_stream) r = draw<R>(g, R(0.0), R(1.0));
+                    else r = u01<R>(w.x);
+                    refl = reflectance(cos_theta, ri) > r;
+                }
+                dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
+            } else {
+                V<R> rs;
+                if constexpr (G::exact_stream) rs = random_in_unit_sphere<R>(g);
+                else rs = unit_ball_inverse<R>(w.x, w.y, w.z);
+                if (mkind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
+                    dir = h.n + rs;
+                    if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
+                } else {  // metal.rs:73-91 (draws even when fuzz = 0, Q5)
+                    dir = normalize(reflect(ray.d, h.n)) + mparam * rs;
+                    scattered = dot(dir, h.n) > R(0.0);  // else absorbed: emitted = 0
+                }
+                if (scattered) att = albedo();
+            }
+            if (scattered) {
+                tp = tp * att;
+                ray.o = h.p;
+                ray.d = dir;
+                prep_ray<R, EXACT>(ray);
+                bounced = true;
+                ++b;
+                term = false;
+            } else if constexpr (!G::exact_stream) {
+                w = g.block(cur + 1, 0u);  // absorbed by a metal: the next sample's camera block
             }
         }
         if (term) {
