@@ -912,8 +912,14 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // PROF (diagnostic builds only, never timed): per-wave s_memtime stamps split
 // each loop iteration into camera-ray / trace / shading cycles, summed into
 // p.counters[0..3] = {iterations, camera, trace, shade} (+ [4] waves).
+// Register budget: the f32 world-mode Philox kernel sits at the 80-VGPR edge of
+// 6 waves per SIMD; ask for 6 (the other variants keep the compiler's choice).
+template <typename R, class G, int MAXD>
+constexpr int min_waves_per_simd() { return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds) ? 6 : 1; }
+
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF = false>
-__global__ void __launch_bounds__(BLOCK) render_kernel(const RenderParams p, const DSceneView<R> gsc) {
+__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>()))
+render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][4];
     if constexpr (PROF) {
