@@ -138,10 +138,12 @@ def main():
     scene.upload(local)
     t_upload = time.perf_counter() - t0
 
-    rows_max = (H + world - 1) // world
+    from nrt import shard
+
+    rows_max = shard.rows_max(H, world)
     rows = scene.rows_selected(H, rank, world)
+    assert rows == shard.rows_of(H, rank, world)
     buf = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(buf) for _ in range(world)] if (rank == 0 and world > 1) else None
     final = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
     stream = torch.cuda.current_stream()
     ev = []
@@ -154,10 +156,8 @@ def main():
         e1.record(stream)
         if timed:
             ev.append((e0, e1))
-        if world > 1:
-            dist.gather(buf, gather_list=gather, dst=0)  # the single RCCL collective
-            if rank == 0:  # rows r, r+N, ... of rank r -> final image rows
-                final.copy_(torch.stack(gather, 0).transpose(0, 1).reshape(rows_max * world, W, 3)[:H])
+        if world > 1:  # the single RCCL collective + un-permute on rank 0
+            shard.gather_frame(buf, H, dist, rank, world, out=final)
 
     for _ in range(args.warmup):
         step(False)
