@@ -23,6 +23,7 @@ LOADABLE = [
     ("scenes/quads.toml", dict()),
     ("scenes/cornell-box-model.json", dict(width=8, height=8)),
     ("scenes/cube-model.toml", dict(width=8, height=8)),
+    ("scenes/utah-teapot-scene.json", dict(width=64, height=64, spp=4)),  # generated model (Q16)
 ]
 
 
@@ -91,7 +92,6 @@ def test_spheres_counts():
 
 
 @pytest.mark.parametrize("scene,code", [
-    ("scenes/utah-teapot-scene.json", -2),   # utah-teapot-model.toml absent in the reference (Q16)
     ("scenes/triangles.toml", -2),           # legacy schema (Q14)
     ("scenes/noise.toml", -4),               # Perlin textures: outside the accelerated path
     ("scenes/simple-lights.toml", -4),
