@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--rng", default="philox", choices=["chacha8", "philox"])
-    ap.add_argument("--trace", default="auto", choices=["auto", "bvh", "world-list"],
+    ap.add_argument("--trace", default="auto", choices=["auto", "bvh", "world-list", "world-bvh"],
                     help="f32 kernel traversal (nrt_trace): auto = world-space list for small flattenable scenes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)

@@ -35,10 +35,14 @@ enum {
 enum nrt_precision { NRT_PRECISION_F64 = 0, NRT_PRECISION_F32 = 1 };
 enum nrt_rng { NRT_RNG_CHACHA8 = 0, NRT_RNG_PHILOX = 1 };
 /* Traversal of the f32 kernel (the f64 kernel always walks the reference's BVH):
- * AUTO picks WORLD_LIST for scenes whose primitives all flatten to world space
- * and make at most NRT_WORLD_LIST_MAX test units (nrt_scene_stats.world_prims), else BVH (instances kept, per-lane
- * traversal).  WORLD_LIST fails with NRT_E_INVALID on scenes that cannot flatten. */
-enum nrt_trace { NRT_TRACE_AUTO = 0, NRT_TRACE_BVH = 1, NRT_TRACE_WORLD_LIST = 2 };
+ *   BVH        the reference's BVH with instances kept (composed transforms), per lane;
+ *   WORLD_LIST instances flattened to world space, every lane tests every primitive
+ *              (six quads closing a box count as one slab test);
+ *   WORLD_BVH  instances flattened, binned-SAH BVH, nearest-child-first with a per-lane stack.
+ * AUTO picks WORLD_LIST when the scene flattens and makes at most NRT_WORLD_LIST_MAX
+ * test units (nrt_scene_stats.world_prims), else WORLD_BVH when it flattens, else BVH.
+ * The WORLD_* modes fail with NRT_E_INVALID on scenes that cannot flatten. */
+enum nrt_trace { NRT_TRACE_AUTO = 0, NRT_TRACE_BVH = 1, NRT_TRACE_WORLD_LIST = 2, NRT_TRACE_WORLD_BVH = 3 };
 #define NRT_WORLD_LIST_MAX 48
 
 typedef struct nrt_scene nrt_scene;

@@ -191,7 +191,7 @@ void check_opts(const nrt_render_opts* o) {
     if (!o) return;
     if (o->precision > NRT_PRECISION_F32) throw std::invalid_argument("unknown precision");
     if (o->rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
-    if (o->trace > NRT_TRACE_WORLD_LIST) throw std::invalid_argument("unknown trace mode");
+    if (o->trace > NRT_TRACE_WORLD_BVH) throw std::invalid_argument("unknown trace mode");
 }
 
 }  // namespace

@@ -105,6 +105,22 @@ constexpr uint32_t BOX_ENTRIES = 7;
 // BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised
 // without reordering candidates.
 
+// Fast kernel, world-BVH mode (large flattenable scenes): a binary BVH over the
+// world-space primitives built with binned SAH on the host.  Each node holds
+// both children's boxes so one visit tests two boxes and descends into the
+// nearer hit child first (the farther one goes on a per-lane LDS stack).
+// Child refs: >= 0 inner node index; < 0 leaf, ~ref = first << 3 | (count - 1)
+// over the BVH-ordered primitive array (count 1..8).
+struct alignas(16) DBvhNode {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t c0, c1;
+    uint32_t pad[2];
+};
+constexpr int32_t WBVH_DONE = INT32_MIN;  // "stack empty" marker (never a valid leaf ref)
+constexpr uint32_t WBVH_STACK = 32;       // per-lane stack entries (host checks the tree depth)
+constexpr uint32_t WBVH_LEAF_MAX = 8;
+
 template <typename Real>
 struct alignas(16) DXform {
     // TRANSLATE: m[0..2] = offset
@@ -180,6 +196,9 @@ struct DSceneView {
     uint32_t n_wprims;
     const uint32_t* wruns;           // runs of same-kind world primitives
     uint32_t n_wruns;
+    const DBvhNode* wbvh;            // world-BVH mode: nodes (wprims then holds the BVH-ordered prims)
+    int32_t wbvh_root;               // child ref of the root
+    uint32_t n_wbvh;
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each

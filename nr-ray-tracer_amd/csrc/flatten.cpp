@@ -544,6 +544,45 @@ struct Flattener {
         }
         if (out.wprims.size() > WORLD_PRIM_CAP) out.world_ok = false;
     }
+    // World BVH over the world primitives (wbvh.hpp); unusable trees (too deep for
+    // the kernel's stack) leave wbvh_ok false and the instance BVH in charge.
+    void build_wbvh() {
+        std::vector<std::array<double, 6>> bounds(out.wprims.size());
+        for (size_t i = 0; i < out.wprims.size(); ++i) {
+            const DPrimWorld<double>& w = out.wprims[i];
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            auto grow = [&](const double* p) {
+                for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+            };
+            const uint32_t kind = w.meta & 3u;
+            if (kind == PRIM_SPHERE) {  // center(t) = N + t * speed, t in [0, 1]
+                for (int end = 0; end < 2; ++end)
+                    for (int sg = -1; sg <= 1; sg += 2) {
+                        double p[3];
+                        for (int k = 0; k < 3; ++k) p[k] = w.N[k] + end * w.AB[k] + sg * std::fabs(w.D);
+                        grow(p);
+                    }
+            } else {
+                const auto& g = wgeom[i];
+                for (int c = 0; c < (kind == PRIM_QUAD ? 4 : 3); ++c) {
+                    double p[3];
+                    for (int k = 0; k < 3; ++k) p[k] = g[0][k] + ((c & 1) ? g[1][k] : 0.0) + ((c & 2) ? g[2][k] : 0.0);
+                    grow(p);
+                }
+            }
+            for (int k = 0; k < 3; ++k) { bounds[i][k] = lo[k]; bounds[i][3 + k] = hi[k]; }
+        }
+        try {
+            out.wbvh = build_world_bvh(bounds);
+        } catch (const std::runtime_error&) {
+            out.wbvh_ok = false;
+            return;
+        }
+        out.wbvh_prims.reserve(out.wbvh.order.size());
+        for (uint32_t idx : out.wbvh.order) out.wbvh_prims.push_back(out.wprims[idx]);
+        out.wbvh_ok = true;
+    }
+
     // DXform of a transform node (every chain was emitted by instance()).
     std::map<const Object*, uint32_t> xform_of;
     uint32_t xform_index(const Object* t) {
@@ -621,6 +660,7 @@ struct Flattener {
         out.world_ok = true;
         world_walk(top, Affine{});
         if (!out.world_ok) out.wprims.clear();
+        if (out.world_ok && !out.wprims.empty()) build_wbvh();
         // fuse closed boxes, then group units into same-kind runs (order kept)
         std::vector<DPrimWorld<double>> fused;
         std::vector<uint32_t> kinds;
@@ -686,15 +726,19 @@ FlatScene32 to_f32(const FlatScene& s) {
         b.d = (float)a.d; b.a0 = (float)a.a0; b.b0 = (float)a.b0;
         b.kind = a.kind; b.material = a.material; b.pad[0] = b.pad[1] = 0;
     }
-    o.wprims.resize(s.wprims.size());
-    for (size_t i = 0; i < s.wprims.size(); ++i) {
-        const auto& a = s.wprims[i];
-        auto& b = o.wprims[i];
-        for (int k = 0; k < 3; ++k) { b.N[k] = (float)a.N[k]; b.S[k] = (float)a.S[k]; }
-        for (int k = 0; k < 8; ++k) b.AB[k] = (float)a.AB[k];
-        b.D = (float)a.D;
-        b.meta = a.meta;
-    }
+    auto world32 = [](const std::vector<DPrimWorld<double>>& src, std::vector<DPrimWorld<float>>& dst) {
+        dst.resize(src.size());
+        for (size_t i = 0; i < src.size(); ++i) {
+            const auto& a = src[i];
+            auto& b = dst[i];
+            for (int k = 0; k < 3; ++k) { b.N[k] = (float)a.N[k]; b.S[k] = (float)a.S[k]; }
+            for (int k = 0; k < 8; ++k) b.AB[k] = (float)a.AB[k];
+            b.D = (float)a.D;
+            b.meta = a.meta;
+        }
+    };
+    world32(s.wprims, o.wprims);
+    world32(s.wbvh_prims, o.wbvh_prims);
     o.inst_fast.resize(s.inst_fast.size());
     for (size_t i = 0; i < s.inst_fast.size(); ++i) {
         const auto& a = s.inst_fast[i];

@@ -6,6 +6,7 @@
 
 #include "device_scene.hpp"
 #include "scene.hpp"
+#include "wbvh.hpp"
 
 namespace nrt {
 
@@ -31,6 +32,10 @@ struct FlatScene {
     std::vector<uint32_t> wruns;  // kind | count << 2 over wprims
     uint64_t world_units = 0;     // primitives + fused boxes: the world list's test count
     bool world_ok = false;
+    // World BVH over the (unfused) world primitives, for large flattenable scenes.
+    WorldBvh wbvh;
+    std::vector<DPrimWorld<double>> wbvh_prims;  // BVH leaf order
+    bool wbvh_ok = false;
 };
 
 FlatScene flatten_scene(const ObjectPtr& top_level_bvh);
@@ -44,6 +49,7 @@ struct FlatScene32 {
     std::vector<DInstFast<float>> inst_fast;
     std::vector<DPrimFast<float>> fprims;
     std::vector<DPrimWorld<float>> wprims;
+    std::vector<DPrimWorld<float>> wbvh_prims;
 };
 FlatScene32 to_f32(const FlatScene& s);
 

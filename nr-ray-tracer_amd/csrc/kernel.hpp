@@ -597,6 +597,97 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     return best >= 0;
 }
 
+// World-BVH mode (MAXD = MODE_WORLD_BVH = -1, fast kernel): per-lane traversal of
+// the binned-SAH tree (device_scene.hpp DBvhNode).  Both children's boxes are
+// tested per visit; the nearer hit child is taken and the farther pushed on the
+// lane's stack (LDS, entry k at stack[k * BLOCK]), so t_best shrinks early and
+// culls the far side.  The lanes of a wave descend until each holds a leaf (or
+// is done) before leaves are tested together ("while-while").
+__device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
+    const uint32_t kind = q.meta & 3u;
+    if (kind == PRIM_SPHERE) {
+        DPrim<float> sp;
+        for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
+        sp.s = q.D;
+        const float t = sphere_t(sp, ray);
+        return (t >= 0.0f && t <= t_best) ? t : -1.0f;
+    }
+    const V<float> nrm = ld3(q.N);
+    const float denom = dot(nrm, ray.d);
+    const float t = (q.D - dot(nrm, ray.o)) * __builtin_amdgcn_rcpf(denom);
+    const V<float> pt = ray.o + t * ray.d;
+    const float alpha = dot(pt, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
+    const float beta = dot(pt, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
+    const float lo = fminf(alpha, beta);
+    const bool inside = kind == PRIM_QUAD ? (lo >= 0.0f) & (alpha <= 1.0f) & (beta <= 1.0f)
+                                          : (lo > 0.0f) & (alpha + beta < 1.0f);
+    const bool ok = (fabsf(denom) >= 1e-8f) & (t >= 0.001f) & (t <= t_best) & inside;
+    return ok ? t : -1.0f;
+}
+
+template <typename T>
+__device__ __forceinline__ T load16(const T* p) {  // whole record, 16-byte loads issued together
+    T r;
+    const uint4* s = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 16); ++k) d[k] = s[k];
+    return r;
+}
+
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm,
+                                                int32_t* stack) {
+    static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
+    const float ix = __builtin_amdgcn_rcpf(ray.d.x), iy = __builtin_amdgcn_rcpf(ray.d.y),
+                iz = __builtin_amdgcn_rcpf(ray.d.z);
+    const float ox = ray.o.x * ix, oy = ray.o.y * iy, oz = ray.o.z * iz;  // slab t = bound * inv - o * inv
+    float t_best = INFINITY;
+    int32_t best = -1;
+    int32_t node = sc.wbvh_root;
+    uint32_t sp = 0;
+    auto pop = [&]() -> int32_t { return sp ? stack[(--sp) * BLOCK] : WBVH_DONE; };
+    while (true) {
+        while (node >= 0) {  // inner node: both child boxes, nearer hit child first
+            const DBvhNode nd = load16(sc.wbvh + node);
+            const float a0x = nd.lo0[0] * ix - ox, b0x = nd.hi0[0] * ix - ox;
+            const float a0y = nd.lo0[1] * iy - oy, b0y = nd.hi0[1] * iy - oy;
+            const float a0z = nd.lo0[2] * iz - oz, b0z = nd.hi0[2] * iz - oz;
+            const float a1x = nd.lo1[0] * ix - ox, b1x = nd.hi1[0] * ix - ox;
+            const float a1y = nd.lo1[1] * iy - oy, b1y = nd.hi1[1] * iy - oy;
+            const float a1z = nd.lo1[2] * iz - oz, b1z = nd.hi1[2] * iz - oz;
+            const float tn0 = fmaxf(fmaxf(fmaxf(fminf(a0x, b0x), fminf(a0y, b0y)), fminf(a0z, b0z)), 0.0f);
+            const float tf0 = fminf(fminf(fminf(fmaxf(a0x, b0x), fmaxf(a0y, b0y)), fmaxf(a0z, b0z)), t_best);
+            const float tn1 = fmaxf(fmaxf(fmaxf(fminf(a1x, b1x), fminf(a1y, b1y)), fminf(a1z, b1z)), 0.0f);
+            const float tf1 = fminf(fminf(fminf(fmaxf(a1x, b1x), fmaxf(a1y, b1y)), fmaxf(a1z, b1z)), t_best);
+            const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+            if (h0 && h1) {
+                const bool near0 = tn0 <= tn1;
+                stack[(sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
+                node = near0 ? nd.c0 : nd.c1;
+            } else if (h0 || h1) {
+                node = h0 ? nd.c0 : nd.c1;
+            } else {
+                node = pop();
+            }
+        }
+        if (node == WBVH_DONE) break;
+        const uint32_t v = ~(uint32_t)node, first = v >> 3, cnt = (v & 7u) + 1u;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const DPrimWorld<float> q = load16(sc.wprims + first + k);
+            const float t = world_prim_t(q, ray, t_best);
+            const bool ok = t >= 0.0f;
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)(first + k) : best;
+        }
+        node = pop();
+    }
+    hm.t = t_best;
+    hm.prim = (uint32_t)best;
+    hm.depth = 0;
+    return best >= 0;
+}
+
 // Closest hit over the flattened scene ("while-while": lanes first run through
 // inner nodes until each holds a leaf, then leaves are processed together).
 // Candidates arrive in the reference's depth-first, left-before-right order,
@@ -703,8 +794,10 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 }
 
 template <typename R, int MAXD, bool EXACT>
-__device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
+                                      int32_t* stack) {
     if constexpr (MAXD == 0) return trace_world(sc, wray, hm);
+    else if constexpr (MAXD < 0) return trace_world_bvh(sc, wray, hm, stack);
     else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
@@ -826,7 +919,7 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
 
 template <typename R, int MAXD, bool EXACT>
 __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
-    if constexpr (MAXD == 0) return make_record_world(sc, wray, hm);
+    if constexpr (MAXD <= 0) return make_record_world(sc, wray, hm);
     else return make_record_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
@@ -916,6 +1009,7 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // 6 waves per SIMD; ask for 6 (the other variants keep the compiler's choice).
 template <typename R, class G, int MAXD>
 constexpr int min_waves_per_simd() { return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds) ? 6 : 1; }
+static_assert(BLOCK % 64 == 0, "stack / ring layouts assume whole waves");
 
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF = false>
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>()))
@@ -931,9 +1025,12 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     auto leader = [&]() {  // first active lane of the wave
         return (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x;
     };
+    // dynamic LDS: [ChaCha8 ring][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
+    constexpr uint32_t stack_bytes = MAXD < 0 ? WBVH_STACK * BLOCK * sizeof(int32_t) : 0;
+    int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
-    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes);
+    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + stack_bytes);
 
     const uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
     if (i >= p.pixel_end) return;
@@ -1015,8 +1112,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
         if (b < p.max_bounces) {  // depth cap returns black (Q6)
             HitMin<R, MAXD> hm;
-            // world mode tests the list through the scalar cache (global view); records read LDS
-            const bool hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm);
+            // world modes traverse the global tables (the list through the scalar cache); records read LDS
+            const bool hit = trace<R, MAXD, EXACT>(MAXD <= 0 ? gsc : sc, ray, hm, stack);
             t2 = stamp();
             if (!hit) {
                 contrib = tp * background;

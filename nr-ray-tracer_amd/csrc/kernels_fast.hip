@@ -8,7 +8,8 @@ namespace nrt {
 
 template <class G>
 static void launch_fast_rng(const RenderParams& p, const DSceneView<float>& v, int maxd, hipStream_t stream) {
-    if (maxd == 0) launch_one<float, G, 0, false>(p, v, stream);
+    if (maxd == MODE_WORLD_BVH) launch_one<float, G, MODE_WORLD_BVH, false>(p, v, stream);
+    else if (maxd == MODE_WORLD_LIST) launch_one<float, G, MODE_WORLD_LIST, false>(p, v, stream);
     else if (maxd == 1) launch_one<float, G, 1, false>(p, v, stream);
     else launch_one<float, G, MAX_INSTANCE_DEPTH, false>(p, v, stream);
 }

@@ -43,6 +43,9 @@ struct DeviceScene {
     size_t bytes = 0;
     bool world_ok = false;  // fast kernel may run in world-space mode (v32.wprims)
     uint64_t world_units = 0;
+    bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
+    const DPrimWorld<float>* wbvh_prims = nullptr;
+    uint32_t n_wbvh_prims = 0;
 };
 
 int gpu_device_count() {
@@ -74,6 +77,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* mfast = (DMatFast*)track(upload(fs.mats_fast, "mats_fast"), fs.mats_fast.size() * sizeof(DMatFast));
         auto* wpr = (DPrimWorld<float>*)track(upload(f32.wprims, "wprims"), f32.wprims.size() * sizeof(DPrimWorld<float>));
         auto* wrn = (uint32_t*)track(upload(fs.wruns, "wruns"), fs.wruns.size() * sizeof(uint32_t));
+        auto* wbn = (DBvhNode*)track(upload(fs.wbvh.nodes, "wbvh"), fs.wbvh.nodes.size() * sizeof(DBvhNode));
+        auto* wbp = (DPrimWorld<float>*)track(upload(f32.wbvh_prims, "wbvh_prims"),
+                                              f32.wbvh_prims.size() * sizeof(DPrimWorld<float>));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
                        ni = (uint32_t)fs.instances.size(), nm = (uint32_t)fs.materials.size(),
                        nt = (uint32_t)fs.textures.size();
@@ -81,13 +87,16 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0, nullptr, 0};
+                                     nullptr, 0, nullptr, 0, nullptr, WBVH_DONE, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
-                                    (uint32_t)fs.wruns.size()};
+                                    (uint32_t)fs.wruns.size(), wbn, fs.wbvh.root, (uint32_t)fs.wbvh.nodes.size()};
+        ds->wbvh_ok = fs.wbvh_ok;
+        ds->wbvh_prims = wbp;
+        ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();
         ds->world_ok = fs.world_ok;
         ds->world_units = fs.world_units;
     } catch (...) {
@@ -110,18 +119,24 @@ void gpu_free_scene(DeviceScene* ds) {
 size_t gpu_scene_bytes(const DeviceScene* ds) { return ds ? ds->bytes : 0; }
 int gpu_scene_device(const DeviceScene* ds) { return ds ? ds->device : -1; }
 
-// Fast kernel traversal mode for `trace` (nrt_render_opts.trace): world-space
+// Fast kernel traversal mode for `trace` (nrt_render_opts.trace): the world
 // list when every primitive could be pulled to world space and the list is
-// short enough that testing all of it beats per-lane BVH traversal.
+// short enough that testing all of it beats traversal; else the world BVH;
+// else (instances that cannot flatten) the instance BVH.
 int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace) {
     const int inst_maxd = ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1;
     if (trace == NRT_TRACE_BVH) return inst_maxd;
     const bool world = ds->world_ok && ds->v32.n_wprims > 0;
     if (trace == NRT_TRACE_WORLD_LIST) {
         if (!world) throw std::invalid_argument("trace=world-list: scene has primitives that cannot be flattened to world space");
-        return 0;
+        return MODE_WORLD_LIST;
     }
-    return (world && ds->world_units <= NRT_WORLD_LIST_MAX) ? 0 : inst_maxd;
+    if (trace == NRT_TRACE_WORLD_BVH) {
+        if (!ds->wbvh_ok) throw std::invalid_argument("trace=world-bvh: scene cannot be flattened to world space");
+        return MODE_WORLD_BVH;
+    }
+    if (world && ds->world_units <= NRT_WORLD_LIST_MAX) return MODE_WORLD_LIST;
+    return ds->wbvh_ok ? MODE_WORLD_BVH : inst_maxd;
 }
 
 void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t precision, uint32_t rng,
@@ -133,8 +148,14 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     else {
         const int maxd = gpu_fast_maxd(ds, trace);
         DSceneView<float> v = ds->v32;  // stage (LDS) only the tables this mode reads
-        if (maxd == 0) {
+        if (maxd == MODE_WORLD_LIST) {
             v.n_nodes = v.n_fprims = v.n_inst_fast = v.n_instances = 0;
+        } else if (maxd == MODE_WORLD_BVH) {
+            v.n_nodes = v.n_fprims = v.n_inst_fast = v.n_instances = 0;
+            v.wprims = ds->wbvh_prims;  // records come from the BVH-ordered array
+            v.n_wprims = ds->n_wbvh_prims;
+            v.wruns = nullptr;
+            v.n_wruns = 0;
         } else {
             v.n_wprims = 0;
         }

@@ -1,0 +1,173 @@
+// Binned-SAH build of the f32 kernel's world BVH (wbvh.hpp).
+//
+// Standard top-down binned SAH (16 bins per axis, all three axes), traversal
+// cost 1, primitive cost 1, leaves of at most WBVH_LEAF_MAX primitives.  The
+// tree is only an acceleration structure of the fast kernel: which primitive
+// is hit does not depend on it (closest hit, f32 statistical parity).
+#include "wbvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <stdexcept>
+
+namespace nrt {
+
+namespace {
+
+struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY};
+    double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+    }
+    void grow(const double* p) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+    }
+    double area() const {
+        if (!(hi[0] >= lo[0])) return 0.0;
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return 2.0 * (x * y + y * z + z * x);
+    }
+};
+
+struct Item {
+    Box box;
+    double c[3];
+    uint32_t index;
+};
+
+struct Builder {
+    std::vector<Item> items;
+    WorldBvh out;
+    double pad = 0.0;
+
+    static constexpr int BINS = 16;
+
+    float down(double x) const {
+        float f = (float)(x - pad);
+        if ((double)f > x - pad) f = std::nextafter(f, -INFINITY);
+        return f;
+    }
+    float up(double x) const {
+        float f = (float)(x + pad);
+        if ((double)f < x + pad) f = std::nextafter(f, INFINITY);
+        return f;
+    }
+
+    Box bounds(size_t b, size_t e) const {
+        Box r;
+        for (size_t i = b; i < e; ++i) r.grow(items[i].box);
+        return r;
+    }
+
+    int32_t leaf(size_t b, size_t e) {
+        const uint32_t first = (uint32_t)out.order.size();
+        if (first >= (1u << 27)) throw std::runtime_error("world BVH: too many primitives");
+        for (size_t i = b; i < e; ++i) out.order.push_back(items[i].index);
+        return ~(int32_t)((first << 3) | (uint32_t)(e - b - 1));
+    }
+
+    // Returns the child ref of items[b, e).
+    int32_t build(size_t b, size_t e, uint32_t depth) {
+        const size_t n = e - b;
+        if (n <= 1) return leaf(b, e);
+        Box cb;  // centroid bounds
+        for (size_t i = b; i < e; ++i) cb.grow(items[i].c);
+        const Box all = bounds(b, e);
+        double best_cost = INFINITY;
+        int best_axis = -1, best_split = 0;
+        for (int a = 0; a < 3; ++a) {
+            const double ext = cb.hi[a] - cb.lo[a];
+            if (!(ext > 0.0)) continue;
+            Box bin_box[BINS];
+            size_t bin_n[BINS] = {};
+            const double scale = BINS / ext;
+            for (size_t i = b; i < e; ++i) {
+                int k = (int)((items[i].c[a] - cb.lo[a]) * scale);
+                k = std::min(std::max(k, 0), BINS - 1);
+                bin_box[k].grow(items[i].box);
+                ++bin_n[k];
+            }
+            double right_area[BINS];
+            size_t right_n[BINS];
+            Box acc;
+            size_t cnt = 0;
+            for (int k = BINS - 1; k > 0; --k) {
+                acc.grow(bin_box[k]);
+                cnt += bin_n[k];
+                right_area[k] = acc.area();
+                right_n[k] = cnt;
+            }
+            acc = Box();
+            cnt = 0;
+            for (int k = 0; k < BINS - 1; ++k) {  // split between bin k and k + 1
+                acc.grow(bin_box[k]);
+                cnt += bin_n[k];
+                if (cnt == 0 || right_n[k + 1] == 0) continue;
+                const double cost = acc.area() * (double)cnt + right_area[k + 1] * (double)right_n[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_split = k;
+                }
+            }
+        }
+        const double leaf_cost = (double)n;
+        const double split_cost = 1.0 + best_cost / std::max(all.area(), 1e-300);
+        size_t mid;
+        if (best_axis < 0) {  // all centroids coincide: split by count
+            if (n <= WBVH_LEAF_MAX) return leaf(b, e);
+            mid = b + n / 2;
+        } else {
+            if (n <= WBVH_LEAF_MAX && leaf_cost <= split_cost) return leaf(b, e);
+            const double ext = cb.hi[best_axis] - cb.lo[best_axis], scale = BINS / ext;
+            auto it = std::partition(items.begin() + b, items.begin() + e, [&](const Item& x) {
+                int k = (int)((x.c[best_axis] - cb.lo[best_axis]) * scale);
+                k = std::min(std::max(k, 0), BINS - 1);
+                return k <= best_split;
+            });
+            mid = (size_t)(it - items.begin());
+            if (mid == b || mid == e) mid = b + n / 2;
+        }
+        if (depth + 1 > out.depth) out.depth = depth + 1;
+        const int32_t idx = (int32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        const int32_t c0 = build(b, mid, depth + 1);
+        const int32_t c1 = build(mid, e, depth + 1);
+        const Box b0 = bounds(b, mid), b1 = bounds(mid, e);
+        DBvhNode& nd = out.nodes[idx];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo0[k] = down(b0.lo[k]); nd.hi0[k] = up(b0.hi[k]);
+            nd.lo1[k] = down(b1.lo[k]); nd.hi1[k] = up(b1.hi[k]);
+        }
+        nd.c0 = c0;
+        nd.c1 = c1;
+        return idx;
+    }
+};
+
+}  // namespace
+
+WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds) {
+    Builder bld;
+    bld.items.resize(bounds.size());
+    double scale = 0.0;
+    for (size_t i = 0; i < bounds.size(); ++i) {
+        Item& it = bld.items[i];
+        for (int k = 0; k < 3; ++k) {
+            it.box.lo[k] = bounds[i][k];
+            it.box.hi[k] = bounds[i][3 + k];
+            it.c[k] = 0.5 * (it.box.lo[k] + it.box.hi[k]);
+            if (std::isfinite(it.box.lo[k])) scale = std::max(scale, std::fabs(it.box.lo[k]));
+            if (std::isfinite(it.box.hi[k])) scale = std::max(scale, std::fabs(it.box.hi[k]));
+        }
+        it.index = (uint32_t)i;
+    }
+    bld.pad = 1e-6 * std::max(scale, 1e-30);  // flat (axis-plane) primitives keep a volume
+    if (!bounds.empty()) bld.out.root = bld.build(0, bld.items.size(), 0);
+    if (bld.out.depth > WBVH_STACK) throw std::runtime_error("world BVH deeper than the kernel's stack");
+    return std::move(bld.out);
+}
+
+}  // namespace nrt

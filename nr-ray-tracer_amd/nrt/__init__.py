@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(_HERE, "libnrt.so")
 
 PRECISION = {"f64": 0, "f32": 1}
 RNG = {"chacha8": 0, "philox": 1}
-TRACE = {"auto": 0, "bvh": 1, "world-list": 2}  # nrt_trace (f32 kernel traversal)
+TRACE = {"auto": 0, "bvh": 1, "world-list": 2, "world-bvh": 3}  # nrt_trace (f32 kernel traversal)
 
 NRT_OK = 0
 ERRORS = {-1: "invalid argument", -2: "load error", -3: "device error", -4: "unsupported"}

@@ -1,0 +1,18 @@
+# Bench every BASELINE config that runs on one GPU (C2, C4, C5; C3 once JPEG decode lands).
+# usage: bash scripts/configs_bench.sh <tag>
+set -o pipefail
+tag=${1:-cfg}
+mkdir -p gpurun_out
+run() {  # name, args...
+  local name=$1; shift
+  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${tag}_$name.json 2> gpurun_out/${tag}_$name.err || { echo "bench $name failed rc=$?"; tail -3 gpurun_out/${tag}_$name.err; return 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'Msamples/s', d['roofline']['kernel_ms'], 'ms', d['config'].get('trace'), d['config'].get('world_prims'))" gpurun_out/${tag}_$name.json $name
+}
+run c2_f32 --scene scenes/cornell-box-scene.json --width 512 --height 512 --spp 64 && \
+run c4_f32 --scene scenes/utah-teapot-scene.json && \
+run c4_f32_chacha --scene scenes/utah-teapot-scene.json --rng chacha8 && \
+run c4_f64 --scene scenes/utah-teapot-scene.json --precision f64 --rng chacha8 --spp 16 && \
+run c1_f32 --scene scenes/spheres.toml --width 400 --height 225 --spp 16 && \
+run c1_f32_big --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 && \
+run c5_f32 && \
+run c5_f32_bvh --trace bvh

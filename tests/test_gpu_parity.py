@@ -161,16 +161,16 @@ def test_empty_and_degenerate_inputs():
     assert np.all(np.isfinite(one.render(precision="f64")))
 
 
-@pytest.mark.parametrize("scene,w,h", [(c[0], c[1], c[2]) for c in CASES_F64[:5]])
+@pytest.mark.parametrize("scene,w,h", [(c[0], c[1], c[2]) for c in CASES_F64[:5] + CASES_F64[7:]])
 @pytest.mark.parametrize("bounces", [1, 2, 3])
-@pytest.mark.parametrize("trace", ["bvh", "world-list"])
+@pytest.mark.parametrize("trace", ["bvh", "world-list", "world-bvh"])
 def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
     """The f32 kernel (leaf lists + composed instance transforms, or the
     world-space list) must follow the same paths as the exact kernel on the
     same ChaCha8 stream: with few bounces any geometry bug shows as whole faces
     of mismatching pixels, while genuine f32 rounding flips stay rare."""
     s = load(scene, w, h, 1, bounces)
-    if trace == "world-list" and s.stats()["world_prims"] == 0:
+    if trace != "bvh" and s.stats()["world_prims"] == 0:
         pytest.skip("scene does not flatten to world space")
     a = s.render(precision="f32", rng="chacha8", trace=trace)
     b = s.render(precision="f64", rng="chacha8")
