@@ -175,6 +175,11 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         for (int q = 0; q < 7; ++q) p.camf[q][k] = (float)vs[q][k];
         if (c.defocus_disk_u[k] != 0.0 || c.defocus_disk_v[k] != 0.0) p.defocus = 1;
     }
+    p.wave_wait = 8;   // world-BVH shading-round threshold (tuning knob: NRT_WAVE_WAIT, 1..64)
+    if (const char* e = std::getenv("NRT_WAVE_WAIT")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 64) p.wave_wait = (uint32_t)v;
+    }
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;

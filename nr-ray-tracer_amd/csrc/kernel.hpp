@@ -635,57 +635,80 @@ __device__ __forceinline__ T load16(const T* p) {  // whole record, 16-byte load
     return r;
 }
 
+// Traversal state of one lane's world-BVH query (kept in registers; the stack in LDS).
+struct WbvhTrav {
+    int32_t node;
+    uint32_t sp;
+    float t_best;
+    int32_t best;
+    float ix, iy, iz, ox, oy, oz;  // 1/d and o/d: slab t = bound * inv - o * inv
+};
+
+__device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray<float>& ray) {
+    ts.ix = __builtin_amdgcn_rcpf(ray.d.x);
+    ts.iy = __builtin_amdgcn_rcpf(ray.d.y);
+    ts.iz = __builtin_amdgcn_rcpf(ray.d.z);
+    ts.ox = ray.o.x * ts.ix;
+    ts.oy = ray.o.y * ts.iy;
+    ts.oz = ray.o.z * ts.iz;
+    ts.node = root;
+    ts.sp = 0;
+    ts.t_best = INFINITY;
+    ts.best = -1;
+}
+
+// One while-while round: descend through inner nodes (nearer hit child first,
+// farther pushed) until the lane holds a leaf or is done, then test the leaf.
+template <typename R>
+__device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                           int32_t* stack) {
+    auto pop = [&]() -> int32_t { return ts.sp ? stack[(--ts.sp) * BLOCK] : WBVH_DONE; };
+    while (ts.node >= 0) {
+        const DBvhNode nd = load16(sc.wbvh + ts.node);
+        const float a0x = nd.lo0[0] * ts.ix - ts.ox, b0x = nd.hi0[0] * ts.ix - ts.ox;
+        const float a0y = nd.lo0[1] * ts.iy - ts.oy, b0y = nd.hi0[1] * ts.iy - ts.oy;
+        const float a0z = nd.lo0[2] * ts.iz - ts.oz, b0z = nd.hi0[2] * ts.iz - ts.oz;
+        const float a1x = nd.lo1[0] * ts.ix - ts.ox, b1x = nd.hi1[0] * ts.ix - ts.ox;
+        const float a1y = nd.lo1[1] * ts.iy - ts.oy, b1y = nd.hi1[1] * ts.iy - ts.oy;
+        const float a1z = nd.lo1[2] * ts.iz - ts.oz, b1z = nd.hi1[2] * ts.iz - ts.oz;
+        const float tn0 = fmaxf(fmaxf(fmaxf(fminf(a0x, b0x), fminf(a0y, b0y)), fminf(a0z, b0z)), 0.0f);
+        const float tf0 = fminf(fminf(fminf(fmaxf(a0x, b0x), fmaxf(a0y, b0y)), fmaxf(a0z, b0z)), ts.t_best);
+        const float tn1 = fmaxf(fmaxf(fmaxf(fminf(a1x, b1x), fminf(a1y, b1y)), fminf(a1z, b1z)), 0.0f);
+        const float tf1 = fminf(fminf(fminf(fmaxf(a1x, b1x), fmaxf(a1y, b1y)), fmaxf(a1z, b1z)), ts.t_best);
+        const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+        if (h0 && h1) {
+            const bool near0 = tn0 <= tn1;
+            stack[(ts.sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
+            ts.node = near0 ? nd.c0 : nd.c1;
+        } else if (h0 || h1) {
+            ts.node = h0 ? nd.c0 : nd.c1;
+        } else {
+            ts.node = pop();
+        }
+    }
+    if (ts.node == WBVH_DONE) return;
+    const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const DPrimWorld<float> q = load16(sc.wprims + first + k);
+        const float t = world_prim_t(q, ray, ts.t_best);
+        const bool ok = t >= 0.0f;
+        ts.t_best = ok ? t : ts.t_best;
+        ts.best = ok ? (int32_t)(first + k) : ts.best;
+    }
+    ts.node = pop();
+}
+
 template <typename R, int MAXD>
 __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm,
                                                 int32_t* stack) {
     static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
-    const float ix = __builtin_amdgcn_rcpf(ray.d.x), iy = __builtin_amdgcn_rcpf(ray.d.y),
-                iz = __builtin_amdgcn_rcpf(ray.d.z);
-    const float ox = ray.o.x * ix, oy = ray.o.y * iy, oz = ray.o.z * iz;  // slab t = bound * inv - o * inv
-    float t_best = INFINITY;
-    int32_t best = -1;
-    int32_t node = sc.wbvh_root;
-    uint32_t sp = 0;
-    auto pop = [&]() -> int32_t { return sp ? stack[(--sp) * BLOCK] : WBVH_DONE; };
-    while (true) {
-        while (node >= 0) {  // inner node: both child boxes, nearer hit child first
-            const DBvhNode nd = load16(sc.wbvh + node);
-            const float a0x = nd.lo0[0] * ix - ox, b0x = nd.hi0[0] * ix - ox;
-            const float a0y = nd.lo0[1] * iy - oy, b0y = nd.hi0[1] * iy - oy;
-            const float a0z = nd.lo0[2] * iz - oz, b0z = nd.hi0[2] * iz - oz;
-            const float a1x = nd.lo1[0] * ix - ox, b1x = nd.hi1[0] * ix - ox;
-            const float a1y = nd.lo1[1] * iy - oy, b1y = nd.hi1[1] * iy - oy;
-            const float a1z = nd.lo1[2] * iz - oz, b1z = nd.hi1[2] * iz - oz;
-            const float tn0 = fmaxf(fmaxf(fmaxf(fminf(a0x, b0x), fminf(a0y, b0y)), fminf(a0z, b0z)), 0.0f);
-            const float tf0 = fminf(fminf(fminf(fmaxf(a0x, b0x), fmaxf(a0y, b0y)), fmaxf(a0z, b0z)), t_best);
-            const float tn1 = fmaxf(fmaxf(fmaxf(fminf(a1x, b1x), fminf(a1y, b1y)), fminf(a1z, b1z)), 0.0f);
-            const float tf1 = fminf(fminf(fminf(fmaxf(a1x, b1x), fmaxf(a1y, b1y)), fmaxf(a1z, b1z)), t_best);
-            const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
-            if (h0 && h1) {
-                const bool near0 = tn0 <= tn1;
-                stack[(sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
-                node = near0 ? nd.c0 : nd.c1;
-            } else if (h0 || h1) {
-                node = h0 ? nd.c0 : nd.c1;
-            } else {
-                node = pop();
-            }
-        }
-        if (node == WBVH_DONE) break;
-        const uint32_t v = ~(uint32_t)node, first = v >> 3, cnt = (v & 7u) + 1u;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const DPrimWorld<float> q = load16(sc.wprims + first + k);
-            const float t = world_prim_t(q, ray, t_best);
-            const bool ok = t >= 0.0f;
-            t_best = ok ? t : t_best;
-            best = ok ? (int32_t)(first + k) : best;
-        }
-        node = pop();
-    }
-    hm.t = t_best;
-    hm.prim = (uint32_t)best;
+    WbvhTrav ts;
+    wbvh_begin(ts, sc.wbvh_root, ray);
+    while (ts.node != WBVH_DONE) wbvh_round(ts, sc, ray, stack);
+    hm.t = ts.t_best;
+    hm.prim = (uint32_t)ts.best;
     hm.depth = 0;
-    return best >= 0;
+    return ts.best >= 0;
 }
 
 // Closest hit over the flattened scene ("while-while": lanes first run through
@@ -1052,56 +1075,58 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
 
     double ax = 0.0, ay = 0.0, az = 0.0;
     uint32_t s = 0, b = 0, cur = 0;  // samples started, bounces of this path, current sample
-    bool fresh = true, bounced = false;
+    bool bounced = false;
     Ray<R> ray;
     V<R> tp = mk(R(1), R(1), R(1));
-    // Philox mode: the block this lane consumes next (exactly one per loop
-    // iteration, computed by every lane at the same point: no divergent refills)
+    // Philox mode: the block this lane consumes next (exactly one per path segment,
+    // computed by every shading lane at the same point: no divergent refills)
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
     if constexpr (!G::exact_stream) w = g.block(0u, 0u);
-    while (true) {
-        const unsigned long long t0 = stamp();
-        if (fresh) {
-            if (s >= p.spp) break;
-            g.start_sample(s);
-            cur = s++;
-            // Camera::get_ray (camera.rs:244-267)
-            R ox = R(0), oy = R(0);
-            if constexpr (G::exact_stream) {
-                if (p.spp > 1) {
-                    ox = draw<R>(g, R(-0.5), R(0.5));
-                    oy = draw<R>(g, R(-0.5), R(0.5));
-                }
-            } else if (p.spp > 1) {
-                ox = u01<R>(w.x) - R(0.5);
-                oy = u01<R>(w.y) - R(0.5);
+
+    // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
+    auto camera_ray = [&]() -> bool {
+        if (s >= p.spp) return false;
+        g.start_sample(s);
+        cur = s++;
+        R ox = R(0), oy = R(0);
+        if constexpr (G::exact_stream) {
+            if (p.spp > 1) {
+                ox = draw<R>(g, R(-0.5), R(0.5));
+                oy = draw<R>(g, R(-0.5), R(0.5));
             }
-            const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
-            if constexpr (G::exact_stream) {
-                const V<R> disk = random_in_unit_disk<R>(g);
-                ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
-                ray.d = point - ray.o;
-                ray.time = draw<R>(g, R(0.0), R(1.0));
-            } else {
-                if (p.defocus) {
-                    const uint4 wd = g.block(cur, PHILOX_STEP_DEFOCUS);
-                    const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
-                    ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
-                } else {
-                    ray.o = look_from;  // zero disk: the draws would only scale zero vectors
-                }
-                ray.d = point - ray.o;
-                ray.time = u01<R>(w.z);
-            }
-            prep_ray<R, EXACT>(ray);
-            tp = mk(R(1), R(1), R(1));
-            b = 0;
-            bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
-            fresh = false;
+        } else if (p.spp > 1) {
+            ox = u01<R>(w.x) - R(0.5);
+            oy = u01<R>(w.y) - R(0.5);
         }
-        const unsigned long long t1 = stamp();
-        unsigned long long t2 = t1;
-        // one step of get_ray_color (camera.rs:269-300): L = a0*(a1*(...*T))
+        const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
+        if constexpr (G::exact_stream) {
+            const V<R> disk = random_in_unit_disk<R>(g);
+            ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+            ray.d = point - ray.o;
+            ray.time = draw<R>(g, R(0.0), R(1.0));
+        } else {
+            if (p.defocus) {
+                const uint4 wd = g.block(cur, PHILOX_STEP_DEFOCUS);
+                const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
+                ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+            } else {
+                ray.o = look_from;  // zero disk: the draws would only scale zero vectors
+            }
+            ray.d = point - ray.o;
+            ray.time = u01<R>(w.z);
+        }
+        prep_ray<R, EXACT>(ray);
+        tp = mk(R(1), R(1), R(1));
+        b = 0;
+        bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
+        return true;
+    };
+
+    // One step of get_ray_color (camera.rs:269-300), L = a0*(a1*(...*T)), after the
+    // closest-hit query of `ray` (`traced` false: the depth cap returned black, Q6).
+    // Returns true when the path continues with a new `ray`; otherwise the sample's
+    // radiance has been added to the pixel sum.
+    auto shade = [&](bool traced, bool hit, const HitMin<R, MAXD>& hm) -> bool {
         bool term = true, scatter = false;
         V<R> contrib = mk(R(0), R(0), R(0));
         Rec<R> h;
@@ -1110,11 +1135,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         bool msolid = false;
         V<R> mcolor = mk(R(0), R(0), R(0));
         auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
-        if (b < p.max_bounces) {  // depth cap returns black (Q6)
-            HitMin<R, MAXD> hm;
-            // world modes traverse the global tables (the list through the scalar cache); records read LDS
-            const bool hit = trace<R, MAXD, EXACT>(MAXD <= 0 ? gsc : sc, ray, hm, stack);
-            t2 = stamp();
+        if (traced) {
             if (!hit) {
                 contrib = tp * background;
             } else {
@@ -1140,7 +1161,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 }
             }
         }
-        // Philox: this iteration's block -- the scatter's (pixel, sample, bounce + 1), or, when
+        // Philox: this segment's block -- the scatter's (pixel, sample, bounce + 1), or, when
         // the path ends here, the next sample's camera block (pixel, sample + 1, 0)
         if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + 1, scatter ? b + 1 : 0u);
         if (scatter) {
@@ -1177,7 +1198,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 tp = tp * att;
                 ray.o = h.p;
                 ray.d = dir;
-                prep_ray<R, EXACT>(ray);
+                if constexpr (MAXD > 0) prep_ray<R, EXACT>(ray);  // world modes need no 1/d here
                 bounced = true;
                 ++b;
                 term = false;
@@ -1189,15 +1210,78 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             ax += (double)contrib.x;
             ay += (double)contrib.y;
             az += (double)contrib.z;
-            fresh = true;
         }
-        if constexpr (PROF) {
-            const unsigned long long t3 = stamp();
-            if (leader()) {
-                atomicAdd(&prof[wave][0], 1ull);
-                atomicAdd(&prof[wave][1], t1 - t0);
-                atomicAdd(&prof[wave][2], t2 - t1);
-                atomicAdd(&prof[wave][3], t3 - t2);
+        return !term;
+    };
+
+    if constexpr (MAXD < 0) {
+        // World-BVH mode: traversal lengths differ widely between lanes, so each lane
+        // keeps its traversal state across rounds; the wave traverses until a ballot
+        // shows at least p.wave_wait lanes finished, then only those lanes shade and
+        // start their next segment (active-ray compaction within the wave).
+        static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
+        WbvhTrav ts;
+        bool active = camera_ray();
+        auto begin = [&]() {
+            if (b < p.max_bounces) wbvh_begin(ts, gsc.wbvh_root, ray);
+            else ts.node = WBVH_DONE;  // depth cap: shaded as black without a query (Q6)
+        };
+        if (active) begin();
+        const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
+        while (true) {
+            const unsigned long long t0 = stamp();
+            while (true) {
+                const bool going = active && ts.node != WBVH_DONE;
+                if (__ballot(going) == 0ull) break;
+                if ((uint32_t)__popcll(__ballot(active && ts.node == WBVH_DONE)) >= wait_min) break;
+                if (going) wbvh_round(ts, gsc, ray, stack);
+            }
+            const unsigned long long t1 = stamp();
+            if (active && ts.node == WBVH_DONE) {
+                HitMin<R, MAXD> hm;
+                hm.t = ts.t_best;
+                hm.prim = (uint32_t)ts.best;
+                hm.depth = 0;
+                if (!shade(b < p.max_bounces, ts.best >= 0, hm)) active = camera_ray();
+                if (active) begin();
+            }
+            if constexpr (PROF) {
+                const unsigned long long t2 = stamp();
+                if (leader()) {
+                    atomicAdd(&prof[wave][0], 1ull);
+                    atomicAdd(&prof[wave][2], t1 - t0);
+                    atomicAdd(&prof[wave][3], t2 - t1);
+                }
+            }
+            if (__ballot(active) == 0ull) break;
+        }
+    } else {
+        bool fresh = true;
+        while (true) {
+            const unsigned long long t0 = stamp();
+            if (fresh) {
+                if (!camera_ray()) break;
+                fresh = false;
+            }
+            const unsigned long long t1 = stamp();
+            unsigned long long t2 = t1;
+            HitMin<R, MAXD> hm;
+            bool hit = false;
+            const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
+            if (traced) {
+                // world list: the global tables through the scalar cache; records read LDS
+                hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                t2 = stamp();
+            }
+            fresh = !shade(traced, hit, hm);
+            if constexpr (PROF) {
+                const unsigned long long t3 = stamp();
+                if (leader()) {
+                    atomicAdd(&prof[wave][0], 1ull);
+                    atomicAdd(&prof[wave][1], t1 - t0);
+                    atomicAdd(&prof[wave][2], t2 - t1);
+                    atomicAdd(&prof[wave][3], t3 - t2);
+                }
             }
         }
     }

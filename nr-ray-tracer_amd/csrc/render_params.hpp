@@ -21,6 +21,7 @@ struct RenderParams {
     // they stay in SGPRs instead of being converted per lane.
     float camf[7][3];
     uint32_t defocus;  // 0: defocus disk is zero (defocus_angle <= 0), disk draws only feed the origin
+    uint32_t wave_wait;  // world-BVH mode: lanes that must finish traversal before a shading round
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;
