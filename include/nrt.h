@@ -195,6 +195,10 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out);
 int nrt_scene_dump(const nrt_scene* scene, char* buf, size_t cap, size_t* needed);
 void nrt_scene_destroy(nrt_scene* scene);
 
+/* Image::try_from_path -> into_rgb32f (lib/textures/image.rs:24-28): decode an image file
+ * (baseline JPEG) to W*H*3 f32 in [0, 1].  Call with rgb = NULL to get the size. */
+int nrt_image_load(const char* path, uint32_t* width, uint32_t* height, float* rgb, size_t cap);
+
 /* gamma_correction + to_rgb8 (lib/image.rs:53-57; image crate Rgb32F->Rgb8). */
 int nrt_image_to_rgb8(const float* rgb, size_t n_floats, float gamma, uint8_t* out);
 

@@ -471,6 +471,20 @@ int nrt_scene_dump(const nrt_scene* scene, char* buf, size_t cap, size_t* needed
 
 void nrt_scene_destroy(nrt_scene* scene) { delete scene; }
 
+int nrt_image_load(const char* path, uint32_t* width, uint32_t* height, float* rgb, size_t cap) {
+    return guarded(NRT_E_LOAD, [&]() {
+        if (!path || !width || !height) throw std::invalid_argument("null argument");
+        const DecodedImage img = decode_image_file(path);
+        *width = img.width;
+        *height = img.height;
+        if (rgb) {
+            if (cap < img.rgb.size()) throw std::invalid_argument("output buffer too small");
+            std::memcpy(rgb, img.rgb.data(), img.rgb.size() * sizeof(float));
+        }
+        return NRT_OK;
+    });
+}
+
 int nrt_image_to_rgb8(const float* rgb, size_t n, float gamma, uint8_t* out) {
     return guarded(NRT_E_INVALID, [&]() {
         if ((n && !rgb) || (n && !out)) throw std::invalid_argument("null argument");

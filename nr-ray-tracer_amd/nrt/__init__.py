@@ -87,6 +87,8 @@ SIGNATURES = {
     "nrt_texture_solid": (C.c_int32, [C.c_void_p, _D3]),
     "nrt_texture_image": (C.c_int32, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "nrt_texture_image_file": (C.c_int32, [C.c_void_p, C.c_char_p]),
+    "nrt_image_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
+                                 C.c_size_t]),
     "nrt_texture_checker": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_double]),
     "nrt_material_lambertian": (C.c_int32, [C.c_void_p, C.c_int32]),
     "nrt_material_metal": (C.c_int32, [C.c_void_p, C.c_double, C.c_int32]),
@@ -441,6 +443,16 @@ class Builder:
         h = C.c_void_p()
         _check(lib().nrt_builder_finish(self._b, bvh, C.byref(h)))
         return Scene(h.value, camera)
+
+
+def image_load(path: str) -> np.ndarray:
+    """Image::try_from_path(..).into_rgb32f(): (H, W, 3) float32 texels in [0, 1]."""
+    w, h = C.c_uint32(), C.c_uint32()
+    _check(lib().nrt_image_load(os.fsencode(path), C.byref(w), C.byref(h), None, 0))
+    out = np.empty((h.value, w.value, 3), dtype=np.float32)
+    _check(lib().nrt_image_load(os.fsencode(path), C.byref(w), C.byref(h),
+                                out.ctypes.data_as(C.POINTER(C.c_float)), out.size))
+    return out
 
 
 def to_rgb8(img: np.ndarray, gamma: float = 0.5) -> np.ndarray:

@@ -1,4 +1,4 @@
-# Bench every BASELINE config that runs on one GPU (C2, C4, C5; C3 once JPEG decode lands).
+# Bench every BASELINE config that runs on one GPU (C2, C3, C4, C5) plus C1's scene at a GPU size.
 # usage: bash scripts/configs_bench.sh <tag>
 set -o pipefail
 tag=${1:-cfg}
@@ -9,6 +9,8 @@ run() {  # name, args...
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'Msamples/s', d['roofline']['kernel_ms'], 'ms', d['config'].get('trace'), d['config'].get('world_prims'))" gpurun_out/${tag}_$name.json $name
 }
 run c2_f32 --scene scenes/cornell-box-scene.json --width 512 --height 512 --spp 64 && \
+run c3_f32 --scene scenes/earth.toml --width 1920 --height 1080 --spp 128 && \
+run c3_f64 --scene scenes/earth.toml --width 1920 --height 1080 --spp 8 --precision f64 --rng chacha8 && \
 run c4_f32 --scene scenes/utah-teapot-scene.json && \
 run c4_f32_chacha --scene scenes/utah-teapot-scene.json --rng chacha8 && \
 run c4_f64 --scene scenes/utah-teapot-scene.json --precision f64 --rng chacha8 --spp 16 && \

@@ -24,6 +24,7 @@ LOADABLE = [
     ("scenes/cornell-box-model.json", dict(width=8, height=8)),
     ("scenes/cube-model.toml", dict(width=8, height=8)),
     ("scenes/utah-teapot-scene.json", dict(width=64, height=64, spp=4)),  # generated model (Q16)
+    ("scenes/earth.toml", dict(width=64, height=36, spp=2)),              # two 2048x1024 JPEG textures
 ]
 
 
