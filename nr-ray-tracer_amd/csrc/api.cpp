@@ -517,7 +517,7 @@ int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, co
             device_sync(dev);
             uint64_t h[8];
             device_copy_to_host(h, ctr, sizeof h, dev);
-            for (size_t k = 0; k < 5; ++k) out[k] = h[k];
+            for (size_t k = 0; k < n && k < 8; ++k) out[k] = h[k];
         } catch (...) {
             device_free(img, dev);
             device_free(ctr, dev);

@@ -30,6 +30,11 @@ enum : uint32_t { NODE_INNER = 0, NODE_PRIM = 1, NODE_INSTANCE = 2, NODE_LIST = 
 // primitive array.  meta = 3 | (count-1) << 2 | first << 8.
 constexpr uint32_t LIST_MAX = 8;
 enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2, PRIM_BOX = 3 /* world mode only */ };
+// World primitives (DPrimWorld, wruns) carry a 3-bit kind: meta = kind | material << 3
+// (box headers: kind | face map << 3), runs = kind | count << 3.  World-list
+// only: quads whose plane normal is a coordinate axis (PRIM_QUAD_X + axis).
+constexpr uint32_t WKIND_BITS = 3, WKIND_MASK = 7;
+enum : uint32_t { PRIM_QUAD_X = 4, PRIM_QUAD_Y = 5, PRIM_QUAD_Z = 6 };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2 };
@@ -93,14 +98,19 @@ struct alignas(16) DPrimWorld {
     Real S[3];      // plane: shading normal (rotations of the chain applied to n)
     uint32_t meta;  // kind | material << 2
 };
+// PRIM_QUAD_X/Y/Z (world list): the plane is x_a = P with a = kind - PRIM_QUAD_X;
+// N[a] = M^T n along the axis, N[(a+1)%3] = P = D / N[a], N[(a+2)%3] = 1e-8 / |N[a]|
+// (the reference's |n.d| >= 1e-8 test as |d_a| >= that), A_a = B_a = 0 with the
+// plane coordinate folded into a0' = a0 - A_a P, b0' = b0 - B_a P.
 // PRIM_BOX (world mode): six consecutive quads that close a parallelepiped
 // {c + a e1 + b e2 + g e3 : a, b, g in [0, 1]} are tested as one slab test in
 // its local frame x' = E^-1 x - E^-1 c.  The header entry holds the rows of
 // E^-1 and E^-1 c as (N, D), (AB[0..2], AB[3]), (AB[4..6], AB[7]); meta =
-// PRIM_BOX | face << 2 with 3 bits per (axis, side) naming which of the six
+// PRIM_BOX | face << 3 with 3 bits per (axis, side) naming which of the six
 // quads that follow the header lies on plane x'_axis = side.  The quads keep
 // their own records (uv, normals, material) for the hit record.
 constexpr uint32_t BOX_ENTRIES = 7;
+constexpr uint32_t WFLAG_AXIS_QUADS = 1;
 // Consecutive units of one kind form a run (kind | count << 2; a box unit is
 // BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised
 // without reordering candidates.
@@ -196,6 +206,7 @@ struct DSceneView {
     uint32_t n_wprims;
     const uint32_t* wruns;           // runs of same-kind world primitives
     uint32_t n_wruns;
+    uint32_t wflags;                 // WFLAG_*: what the world list holds
     const DBvhNode* wbvh;            // world-BVH mode: nodes (wprims then holds the BVH-ordered prims)
     int32_t wbvh_root;               // child ref of the root
     uint32_t n_wbvh;

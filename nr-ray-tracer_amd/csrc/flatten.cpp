@@ -385,12 +385,31 @@ struct Flattener {
     }
     std::vector<std::array<V3a, 3>> wgeom;  // world (p, u, v) of each world prim (quads; zero otherwise)
 
+    // A world quad whose plane normal lies on a coordinate axis -> PRIM_QUAD_X + axis
+    // (device_scene.hpp): plane coordinate, threshold and folded offsets.
+    static void axis_quad(DPrimWorld<double>& w) {
+        int a = -1, zeros = 0;
+        for (int k = 0; k < 3; ++k) {
+            if (w.N[k] == 0.0) ++zeros;
+            else a = k;
+        }
+        if (zeros != 2 || !std::isfinite(w.N[a]) || !std::isfinite(w.D)) return;
+        const double Na = w.N[a], P = w.D / Na;
+        w.AB[6] -= w.AB[2 * a] * P;
+        w.AB[7] -= w.AB[2 * a + 1] * P;
+        w.AB[2 * a] = 0.0;
+        w.AB[2 * a + 1] = 0.0;
+        w.N[(a + 1) % 3] = P;
+        w.N[(a + 2) % 3] = 1e-8 / std::fabs(Na);
+        w.meta = (PRIM_QUAD_X + (uint32_t)a) | (w.meta & ~WKIND_MASK);
+    }
+
     // Six consecutive quads closing a parallelepiped -> PRIM_BOX header (device_scene.hpp).
     bool fuse_box(size_t i, DPrimWorld<double>& hdr) const {
         std::vector<V3a> pts;
         double scale = 0;
         for (size_t q = i; q < i + 6; ++q) {
-            if ((out.wprims[q].meta & 3u) != PRIM_QUAD) return false;
+            if ((out.wprims[q].meta & WKIND_MASK) != PRIM_QUAD) return false;
             const auto& g = wgeom[q];
             const V3a c[4] = {g[0], {g[0][0] + g[1][0], g[0][1] + g[1][1], g[0][2] + g[1][2]},
                               {g[0][0] + g[2][0], g[0][1] + g[2][1], g[0][2] + g[2][2]},
@@ -475,7 +494,7 @@ struct Flattener {
         uint32_t map = 0;
         for (int a = 0; a < 3; ++a)
             for (int sd = 0; sd < 2; ++sd) map |= (uint32_t)face[a][sd] << (3 * (2 * a + sd));
-        hdr.meta = PRIM_BOX | (map << 2);
+        hdr.meta = PRIM_BOX | (map << WKIND_BITS);
         return true;
     }
     static double vdot(const V3a& a, const V3a& c) { return a[0] * c[0] + a[1] * c[1] + a[2] * c[2]; }
@@ -492,7 +511,7 @@ struct Flattener {
                 const V3a c = va(o->center);
                 for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.AB[k] = va(o->speed)[k]; }
                 w.D = o->radius;
-                w.meta = PRIM_SPHERE | (material(o->material) << 2);
+                w.meta = PRIM_SPHERE | (material(o->material) << WKIND_BITS);
                 out.wprims.push_back(w);
                 wgeom.push_back({});
                 break;
@@ -513,7 +532,7 @@ struct Flattener {
                 w.D = o->d - vdot(n, f.b);
                 w.AB[6] = a0 - vdot(Aq, f.b);
                 w.AB[7] = b0 - vdot(Bq, f.b);
-                w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (material(o->material) << 2);
+                w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (material(o->material) << WKIND_BITS);
                 out.wprims.push_back(w);
                 break;
             }
@@ -554,7 +573,7 @@ struct Flattener {
             auto grow = [&](const double* p) {
                 for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
             };
-            const uint32_t kind = w.meta & 3u;
+            const uint32_t kind = w.meta & WKIND_MASK;
             if (kind == PRIM_SPHERE) {  // center(t) = N + t * speed, t in [0, 1]
                 for (int end = 0; end < 2; ++end)
                     for (int sg = -1; sg <= 1; sg += 2) {
@@ -661,29 +680,47 @@ struct Flattener {
         world_walk(top, Affine{});
         if (!out.world_ok) out.wprims.clear();
         if (out.world_ok && !out.wprims.empty()) build_wbvh();
-        // fuse closed boxes, then group units into same-kind runs (order kept)
-        std::vector<DPrimWorld<double>> fused;
-        std::vector<uint32_t> kinds;
+        // fuse closed boxes, then group units by kind: one run per kind.  The f32
+        // kernel's closest hit does not depend on the order except for exact ties
+        // between coincident surfaces (the reference's order is kept within a kind).
+        std::vector<std::vector<DPrimWorld<double>>> units;
+        std::vector<uint32_t> unit_kind;
         for (size_t i = 0; i < out.wprims.size();) {
             DPrimWorld<double> hdr;
             if (i + 6 <= out.wprims.size() && fuse_box(i, hdr)) {
-                fused.push_back(hdr);
-                fused.insert(fused.end(), out.wprims.begin() + i, out.wprims.begin() + i + 6);
-                kinds.push_back(PRIM_BOX);
+                std::vector<DPrimWorld<double>> u{hdr};
+                u.insert(u.end(), out.wprims.begin() + i, out.wprims.begin() + i + 6);
+                units.push_back(std::move(u));
+                unit_kind.push_back(PRIM_BOX);
                 i += 6;
             } else {
-                fused.push_back(out.wprims[i]);
-                kinds.push_back(out.wprims[i].meta & 3u);
+                DPrimWorld<double> w = out.wprims[i];
+                if ((w.meta & WKIND_MASK) == PRIM_QUAD) axis_quad(w);
+                units.push_back({w});
+                unit_kind.push_back(w.meta & WKIND_MASK);
                 ++i;
             }
         }
+        static const int rank[7] = {5, 3, 4, 6, 0, 1, 2};  // X, Y, Z quads, quads, triangles, spheres, boxes
+        std::vector<size_t> order(units.size());
+        for (size_t k = 0; k < order.size(); ++k) order[k] = k;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](size_t a, size_t b) { return rank[unit_kind[a]] < rank[unit_kind[b]]; });
+        std::vector<DPrimWorld<double>> fused;
+        std::vector<uint32_t> kinds;
+        for (size_t k : order) {
+            fused.insert(fused.end(), units[k].begin(), units[k].end());
+            kinds.push_back(unit_kind[k]);
+        }
         out.wprims.swap(fused);
         out.world_units = kinds.size();
+        const uint32_t one = 1u << WKIND_BITS;
         for (uint32_t kind : kinds) {
-            if (!out.wruns.empty() && (out.wruns.back() & 3u) == kind && (out.wruns.back() >> 2) < (1u << 29))
-                out.wruns.back() += 4u;
+            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;
+            if (!out.wruns.empty() && (out.wruns.back() & WKIND_MASK) == kind && (out.wruns.back() >> WKIND_BITS) < (1u << 28))
+                out.wruns.back() += one;
             else
-                out.wruns.push_back(kind | 4u);
+                out.wruns.push_back(kind | one);
         }
     }
 };

@@ -31,6 +31,7 @@ struct FlatScene {
     std::vector<DPrimWorld<double>> wprims;
     std::vector<uint32_t> wruns;  // kind | count << 2 over wprims
     uint64_t world_units = 0;     // primitives + fused boxes: the world list's test count
+    uint32_t wflags = 0;          // WFLAG_* of the world list
     bool world_ok = false;
     // World BVH over the (unfused) world primitives, for large flattenable scenes.
     WorldBvh wbvh;

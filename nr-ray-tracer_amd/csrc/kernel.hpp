@@ -518,15 +518,37 @@ struct HitMin {
     uint32_t inst[MAXD > 0 ? MAXD : 1];
 };
 
-// World-space mode (MAXD = 0, fast kernel): the wave tests every primitive in
-// the reference's depth-first candidate order (`t <= t_best`: the later
-// candidate wins ties, as in trace).  The primitive index is wave-uniform, so
+// World-space mode (MAXD = 0, fast kernel): the wave tests every primitive,
+// grouped by kind (the reference's candidate order within a kind; `t <= t_best`:
+// the later candidate wins ties, as in trace).  The primitive index is wave-uniform, so
 // each record is read once per wave through the scalar cache into SGPRs (the
 // constant address space makes the loads s_load), and no lane diverges.
 template <typename R>
 using ConstPrimWorld = const __attribute__((address_space(4))) DPrimWorld<R>*;
 using ConstU32 = const __attribute__((address_space(4))) uint32_t*;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Axis-aligned quad run (PRIM_QUAD_X + A; device_scene.hpp): t from the per-ray
+// reciprocal, (alpha, beta) from the two in-plane coordinates only.
+template <int A>
+__device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t& k, uint32_t end, const Ray<float>& ray,
+                                              const float inv[3], const float oinv[3], float& t_best, int32_t& best) {
+    constexpr int A1 = (A + 1) % 3, A2 = (A + 2) % 3;
+    const float* o = &ray.o.x;
+    const float* d = &ray.d.x;
+    for (; k < end; ++k) {
+        const ConstPrimWorld<float> q = wp + k;
+        const float t = q->N[A1] * inv[A] - oinv[A];  // (P - o_a) / d_a
+        const float p1 = o[A1] + t * d[A1], p2 = o[A2] + t * d[A2];
+        const f32x2 ab = f32x2{q->AB[2 * A1], q->AB[2 * A1 + 1]} * p1 + f32x2{q->AB[2 * A2], q->AB[2 * A2 + 1]} * p2 -
+                         f32x2{q->AB[6], q->AB[7]};
+        const float lo = fminf(ab.x, ab.y);
+        const bool ok = (fabsf(d[A]) >= q->N[A2]) & (t >= 0.001f) & (t <= t_best) & (lo >= 0.0f) & (ab.x <= 1.0f) &
+                        (ab.y <= 1.0f);
+        t_best = ok ? t : t_best;
+        best = ok ? (int32_t)k : best;
+    }
+}
 
 template <typename R, int MAXD>
 __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
@@ -537,12 +559,23 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     int32_t best = -1;
     // (d, o) pairs: N.d and N.o come out of one packed FMA chain
     const f32x2 dox = {ray.d.x, ray.o.x}, doy = {ray.d.y, ray.o.y}, doz = {ray.d.z, ray.o.z};
+    float inv[3], oinv[3];  // axis-aligned quads: 1/d and o/d
+    if (sc.wflags & WFLAG_AXIS_QUADS) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            inv[a] = __builtin_amdgcn_rcpf((&ray.d.x)[a]);
+            oinv[a] = (&ray.o.x)[a] * inv[a];
+        }
+    }
     uint32_t k = 0;
     for (uint32_t r = 0; r < sc.n_wruns; ++r) {
         const uint32_t run = runs[r];
-        const uint32_t kind = run & 3u, end = k + (run >> 2);
+        const uint32_t kind = run & WKIND_MASK, count = run >> WKIND_BITS, end = k + count;
+        if (kind == PRIM_QUAD_X) { axis_quad_run<0>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
+        if (kind == PRIM_QUAD_Y) { axis_quad_run<1>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
+        if (kind == PRIM_QUAD_Z) { axis_quad_run<2>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
         if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
-            for (uint32_t b = 0; b < (run >> 2); ++b, k += BOX_ENTRIES) {
+            for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
                 const ConstPrimWorld<float> q = wp + k;
                 // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
                 const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
@@ -604,7 +637,7 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
 // culls the far side.  The lanes of a wave descend until each holds a leaf (or
 // is done) before leaves are tested together ("while-while").
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
-    const uint32_t kind = q.meta & 3u;
+    const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
     if (kind == PRIM_SPHERE) {
         DPrim<float> sp;
         for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
@@ -832,11 +865,11 @@ template <typename R, int MAXD>
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
     uint32_t prim = hm.prim;
-    if ((sc.wprims[prim].meta & 3u) == PRIM_BOX) {
+    DPrimWorld<R> q = load16(sc.wprims + prim);
+    const V<R> pw = wray.o + hm.t * wray.d;
+    if ((q.meta & WKIND_MASK) == PRIM_BOX) {
         // which face: the local coordinate of the hit point nearest a face plane
-        const DPrimWorld<R> b = sc.wprims[prim];
-        const V<R> pw = wray.o + hm.t * wray.d;
-        const R l[3] = {dot(ld3(b.N), pw) - b.D, dot(ld3(b.AB), pw) - b.AB[3], dot(ld3(b.AB + 4), pw) - b.AB[7]};
+        const R l[3] = {dot(ld3(q.N), pw) - q.D, dot(ld3(q.AB), pw) - q.AB[3], dot(ld3(q.AB + 4), pw) - q.AB[7]};
         uint32_t slot = 0;
         R dmin = R(INFINITY);
 #pragma unroll
@@ -845,13 +878,14 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
             if (d0 < dmin) { dmin = d0; slot = 2 * a; }
             if (d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
         }
-        prim += 1 + ((b.meta >> (2 + 3 * slot)) & 7u);
+        prim += 1 + ((q.meta >> (WKIND_BITS + 3 * slot)) & 7u);
+        q = load16(sc.wprims + prim);
     }
-    const DPrimWorld<R> q = sc.wprims[prim];
+    const uint32_t kind = q.meta & WKIND_MASK;
     Rec<R> h;
-    h.p = wray.o + hm.t * wray.d;
+    h.p = pw;
     V<R> geo, shade;
-    if ((q.meta & 3u) == PRIM_SPHERE) {
+    if (kind == PRIM_SPHERE) {
         const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
         geo = normalize(h.p - center);
         shade = geo;
@@ -862,13 +896,18 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     } else {
         h.u = dot(h.p, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
         h.v = dot(h.p, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
-        geo = ld3(q.N);
+        if (kind >= PRIM_QUAD_X) {  // axis quad: the normal is N[a] along axis a (other slots hold P, threshold)
+            const uint32_t ax = kind - PRIM_QUAD_X;
+            geo = mk(ax == 0 ? q.N[0] : R(0), ax == 1 ? q.N[1] : R(0), ax == 2 ? q.N[2] : R(0));
+        } else {
+            geo = ld3(q.N);
+        }
         shade = ld3(q.S);
     }
     const R sign = signum(dot(wray.d, geo));
     h.front = sign < R(0);
     h.n = (-sign) * shade;
-    h.mat = q.meta >> 2;
+    h.mat = q.meta >> WKIND_BITS;
     return h;
 }
 
@@ -1038,9 +1077,11 @@ template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF =
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>()))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][4];
+    // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
+    // 6 Philox block, 7 scatter + accumulate
+    __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][8];
     if constexpr (PROF) {
-        if (threadIdx.x < (BLOCK / 64) * 4) prof[threadIdx.x / 4][threadIdx.x % 4] = 0;
+        if (threadIdx.x < (BLOCK / 64) * 8) prof[threadIdx.x / 8][threadIdx.x % 8] = 0;
         __syncthreads();
     }
     const uint32_t wave = threadIdx.x / 64;
@@ -1127,6 +1168,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // Returns true when the path continues with a new `ray`; otherwise the sample's
     // radiance has been added to the pixel sum.
     auto shade = [&](bool traced, bool hit, const HitMin<R, MAXD>& hm) -> bool {
+        const unsigned long long s0 = stamp();
         bool term = true, scatter = false;
         V<R> contrib = mk(R(0), R(0), R(0));
         Rec<R> h;
@@ -1161,9 +1203,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 }
             }
         }
+        const unsigned long long s1 = stamp();
         // Philox: this segment's block -- the scatter's (pixel, sample, bounce + 1), or, when
         // the path ends here, the next sample's camera block (pixel, sample + 1, 0)
         if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + 1, scatter ? b + 1 : 0u);
+        const unsigned long long s2 = stamp();
         if (scatter) {
             V<R> dir;
             V<R> att = mk(R(1), R(1), R(1));
@@ -1210,6 +1254,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             ax += (double)contrib.x;
             ay += (double)contrib.y;
             az += (double)contrib.z;
+        }
+        if constexpr (PROF) {
+            const unsigned long long s3 = stamp();
+            if (leader()) {
+                atomicAdd(&prof[wave][5], s1 - s0);
+                atomicAdd(&prof[wave][6], s2 - s1);
+                atomicAdd(&prof[wave][7], s3 - s2);
+            }
         }
         return !term;
     };
@@ -1287,7 +1339,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     }
     if constexpr (PROF) {
         if (leader()) {
-            for (int c = 0; c < 4; ++c) atomicAdd(&p.counters[c], prof[wave][c]);
+            for (int c = 0; c < 8; ++c)
+                if (c != 4) atomicAdd(&p.counters[c], prof[wave][c]);
             atomicAdd(&p.counters[4], 1ull);
         }
     }

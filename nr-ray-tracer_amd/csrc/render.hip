@@ -87,13 +87,13 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0, nullptr, 0, nullptr, WBVH_DONE, 0};
+                                     nullptr, 0, nullptr, 0, 0, nullptr, WBVH_DONE, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
-                                    (uint32_t)fs.wruns.size(), wbn, fs.wbvh.root, (uint32_t)fs.wbvh.nodes.size()};
+                                    (uint32_t)fs.wruns.size(), fs.wflags, wbn, fs.wbvh.root, (uint32_t)fs.wbvh.nodes.size()};
         ds->wbvh_ok = fs.wbvh_ok;
         ds->wbvh_prims = wbp;
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();

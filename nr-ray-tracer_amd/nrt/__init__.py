@@ -360,12 +360,14 @@ class Scene:
         """Diagnostic render with per-wave stamps: cycle shares of camera / trace / shading."""
         cam = camera or self.camera
         o = _opts(precision, rng, device, 0, 1, trace)
-        out = (C.c_uint64 * 5)()
-        _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 5))
-        iters, cam_c, trace_c, shade_c, waves = list(out)
+        out = (C.c_uint64 * 8)()
+        _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 8))
+        iters, cam_c, trace_c, shade_c, waves, rec_c, rng_c, scat_c = list(out)
         tot = max(cam_c + trace_c + shade_c, 1)
         return {"iterations_per_wave": iters / max(waves, 1), "camera_share": cam_c / tot,
                 "trace_share": trace_c / tot, "shade_share": shade_c / tot,
+                "shade_record_share": rec_c / tot, "shade_rng_share": rng_c / tot,
+                "shade_scatter_share": scat_c / tot,
                 "cycles_per_iteration": tot / max(iters, 1), "waves": waves}
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",
