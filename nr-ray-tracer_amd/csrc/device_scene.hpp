@@ -127,7 +127,22 @@ struct alignas(16) DBvhNode {
     int32_t c0, c1;
     uint32_t pad[2];
 };
+// 4-wide form of the same tree (collapsed on the host), 64 bytes per node:
+// child boxes quantized to 8 bits per plane relative to the node's box,
+// lo_k = org + qlo_k * 2^(e - 127) per axis, rounded outward on the host (the
+// decoded box always contains the f32 child box).  Traversal is gather-bound
+// (each lane loads a different node), so bytes per visit set the speed.
+struct alignas(16) DBvh4Node {
+    float org[3];      // lower corner of the node's box
+    uint32_t exps;     // scale exponent byte per axis (bits 0-7 x, 8-15 y, 16-23 z)
+    uint32_t qlo[3];   // per axis, byte k = child k's low plane
+    uint32_t qhi[3];   // per axis, byte k = child k's high plane
+    int32_t child[4];  // refs as in DBvhNode (inner = DBvh4Node index), WBVH_DONE = empty slot
+    uint32_t pad[2];
+};
+static_assert(sizeof(DBvh4Node) == 64, "one half cache line per 4-wide node");
 constexpr int32_t WBVH_DONE = INT32_MIN;  // "stack empty" marker (never a valid leaf ref)
+constexpr int32_t WBVH_NO_LEAF = 0;       // "no parked leaf" (leaf refs are negative)
 constexpr uint32_t WBVH_STACK = 32;       // per-lane stack entries (host checks the tree depth)
 constexpr uint32_t WBVH_LEAF_MAX = 8;
 
@@ -208,6 +223,8 @@ struct DSceneView {
     uint32_t n_wruns;
     uint32_t wflags;                 // WFLAG_*: what the world list holds
     const DBvhNode* wbvh;            // world-BVH mode: nodes (wprims then holds the BVH-ordered prims)
+    const DBvh4Node* wbvh4;          // the same tree collapsed to 4-wide nodes (root = wbvh4_root)
+    int32_t wbvh4_root;
     int32_t wbvh_root;               // child ref of the root
     uint32_t n_wbvh;
 };

@@ -9,6 +9,10 @@
 #include <map>
 #include <stdexcept>
 
+#ifndef NRT_SPHERE_COST
+#define NRT_SPHERE_COST 4.0f  // SAH weight of an (f64) sphere test relative to a plane test
+#endif
+
 namespace nrt {
 
 namespace {
@@ -567,6 +571,7 @@ struct Flattener {
     // the kernel's stack) leave wbvh_ok false and the instance BVH in charge.
     void build_wbvh() {
         std::vector<std::array<double, 6>> bounds(out.wprims.size());
+        std::vector<float> cost(out.wprims.size(), 1.0f);  // f64 sphere tests cost ~4 plane tests
         for (size_t i = 0; i < out.wprims.size(); ++i) {
             const DPrimWorld<double>& w = out.wprims[i];
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -575,6 +580,7 @@ struct Flattener {
             };
             const uint32_t kind = w.meta & WKIND_MASK;
             if (kind == PRIM_SPHERE) {  // center(t) = N + t * speed, t in [0, 1]
+                cost[i] = NRT_SPHERE_COST;
                 for (int end = 0; end < 2; ++end)
                     for (int sg = -1; sg <= 1; sg += 2) {
                         double p[3];
@@ -592,7 +598,7 @@ struct Flattener {
             for (int k = 0; k < 3; ++k) { bounds[i][k] = lo[k]; bounds[i][3 + k] = hi[k]; }
         }
         try {
-            out.wbvh = build_world_bvh(bounds);
+            out.wbvh = build_world_bvh(bounds, cost);
         } catch (const std::runtime_error&) {
             out.wbvh_ok = false;
             return;

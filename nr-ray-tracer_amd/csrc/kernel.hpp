@@ -28,6 +28,9 @@ namespace nrt {
 namespace dev {
 
 constexpr int BLOCK = 256;
+#ifndef NRT_SPECULATIVE
+#define NRT_SPECULATIVE 1  // world-BVH rounds: lanes holding a leaf keep descending (Aila & Laine)
+#endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 
 template <typename R>
@@ -671,10 +674,12 @@ __device__ __forceinline__ T load16(const T* p) {  // whole record, 16-byte load
 // Traversal state of one lane's world-BVH query (kept in registers; the stack in LDS).
 struct WbvhTrav {
     int32_t node;
+    int32_t leaf;  // parked leaf ref (< 0), WBVH_NO_LEAF when none
     uint32_t sp;
     float t_best;
     int32_t best;
     float ix, iy, iz, ox, oy, oz;  // 1/d and o/d: slab t = bound * inv - o * inv
+    __device__ __forceinline__ bool busy() const { return node != WBVH_DONE || leaf != WBVH_NO_LEAF; }
 };
 
 __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray<float>& ray) {
@@ -685,42 +690,16 @@ __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray
     ts.oy = ray.o.y * ts.iy;
     ts.oz = ray.o.z * ts.iz;
     ts.node = root;
+    ts.leaf = WBVH_NO_LEAF;
     ts.sp = 0;
     ts.t_best = INFINITY;
     ts.best = -1;
 }
 
-// One while-while round: descend through inner nodes (nearer hit child first,
-// farther pushed) until the lane holds a leaf or is done, then test the leaf.
+// Test the primitives of leaf `ref` (world_prim_t, closest hit so far in ts).
 template <typename R>
-__device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                           int32_t* stack) {
-    auto pop = [&]() -> int32_t { return ts.sp ? stack[(--ts.sp) * BLOCK] : WBVH_DONE; };
-    while (ts.node >= 0) {
-        const DBvhNode nd = load16(sc.wbvh + ts.node);
-        const float a0x = nd.lo0[0] * ts.ix - ts.ox, b0x = nd.hi0[0] * ts.ix - ts.ox;
-        const float a0y = nd.lo0[1] * ts.iy - ts.oy, b0y = nd.hi0[1] * ts.iy - ts.oy;
-        const float a0z = nd.lo0[2] * ts.iz - ts.oz, b0z = nd.hi0[2] * ts.iz - ts.oz;
-        const float a1x = nd.lo1[0] * ts.ix - ts.ox, b1x = nd.hi1[0] * ts.ix - ts.ox;
-        const float a1y = nd.lo1[1] * ts.iy - ts.oy, b1y = nd.hi1[1] * ts.iy - ts.oy;
-        const float a1z = nd.lo1[2] * ts.iz - ts.oz, b1z = nd.hi1[2] * ts.iz - ts.oz;
-        const float tn0 = fmaxf(fmaxf(fmaxf(fminf(a0x, b0x), fminf(a0y, b0y)), fminf(a0z, b0z)), 0.0f);
-        const float tf0 = fminf(fminf(fminf(fmaxf(a0x, b0x), fmaxf(a0y, b0y)), fmaxf(a0z, b0z)), ts.t_best);
-        const float tn1 = fmaxf(fmaxf(fmaxf(fminf(a1x, b1x), fminf(a1y, b1y)), fminf(a1z, b1z)), 0.0f);
-        const float tf1 = fminf(fminf(fminf(fmaxf(a1x, b1x), fmaxf(a1y, b1y)), fmaxf(a1z, b1z)), ts.t_best);
-        const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
-        if (h0 && h1) {
-            const bool near0 = tn0 <= tn1;
-            stack[(ts.sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
-            ts.node = near0 ? nd.c0 : nd.c1;
-        } else if (h0 || h1) {
-            ts.node = h0 ? nd.c0 : nd.c1;
-        } else {
-            ts.node = pop();
-        }
-    }
-    if (ts.node == WBVH_DONE) return;
-    const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+__device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
+    const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
     for (uint32_t k = 0; k < cnt; ++k) {
         const DPrimWorld<float> q = load16(sc.wprims + first + k);
         const float t = world_prim_t(q, ray, ts.t_best);
@@ -728,7 +707,134 @@ __device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc
         ts.t_best = ok ? t : ts.t_best;
         ts.best = ok ? (int32_t)(first + k) : ts.best;
     }
-    ts.node = pop();
+}
+
+__device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, const int32_t* stack) {
+    return ts.sp ? stack[(--ts.sp) * BLOCK] : WBVH_DONE;
+}
+
+// Binary node visit: both child boxes, nearer hit child next, the other pushed.
+template <typename R>
+__device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
+    const DBvhNode nd = load16(sc.wbvh + t.node);
+    const float a0x = nd.lo0[0] * t.ix - t.ox, b0x = nd.hi0[0] * t.ix - t.ox;
+    const float a0y = nd.lo0[1] * t.iy - t.oy, b0y = nd.hi0[1] * t.iy - t.oy;
+    const float a0z = nd.lo0[2] * t.iz - t.oz, b0z = nd.hi0[2] * t.iz - t.oz;
+    const float a1x = nd.lo1[0] * t.ix - t.ox, b1x = nd.hi1[0] * t.ix - t.ox;
+    const float a1y = nd.lo1[1] * t.iy - t.oy, b1y = nd.hi1[1] * t.iy - t.oy;
+    const float a1z = nd.lo1[2] * t.iz - t.oz, b1z = nd.hi1[2] * t.iz - t.oz;
+    const float tn0 = fmaxf(fmaxf(fmaxf(fminf(a0x, b0x), fminf(a0y, b0y)), fminf(a0z, b0z)), 0.0f);
+    const float tf0 = fminf(fminf(fminf(fmaxf(a0x, b0x), fmaxf(a0y, b0y)), fmaxf(a0z, b0z)), t.t_best);
+    const float tn1 = fmaxf(fmaxf(fmaxf(fminf(a1x, b1x), fminf(a1y, b1y)), fminf(a1z, b1z)), 0.0f);
+    const float tf1 = fminf(fminf(fminf(fmaxf(a1x, b1x), fmaxf(a1y, b1y)), fmaxf(a1z, b1z)), t.t_best);
+    const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+    if (h0 && h1) {
+        const bool near0 = tn0 <= tn1;
+        stack[(t.sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
+        t.node = near0 ? nd.c0 : nd.c1;
+    } else if (h0 || h1) {
+        t.node = h0 ? nd.c0 : nd.c1;
+    } else {
+        t.node = wbvh_pop(t, stack);
+    }
+}
+
+// 4-wide node visit (DBvh4Node, quantized boxes): hit children sorted by entry
+// distance (5-comparator network), the nearest next, the rest pushed farthest-first.
+__device__ __forceinline__ void wbvh_cswap(float& ta, int32_t& ca, float& tb, int32_t& cb) {
+    const bool sw = tb < ta;
+    const float t0 = ta;
+    const int32_t c0 = ca;
+    ta = sw ? tb : ta;
+    ca = sw ? cb : ca;
+    tb = sw ? t0 : tb;
+    cb = sw ? c0 : cb;
+}
+template <typename R>
+__device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
+    const DBvh4Node nd = load16(sc.wbvh4 + t.node);
+    // plane t = (org + q * step - o) / d = q * (step / d) + (org / d - o / d)
+    const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
+    const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
+    const float Az = __uint_as_float(((nd.exps >> 16) & 0xFFu) << 23) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
+    auto child_t = [&](int k) {  // entry distance of child k, +inf if missed or empty
+        auto q = [&](uint32_t w) { return (float)((w >> (8 * k)) & 0xFFu); };
+        const float ax = q(nd.qlo[0]) * Ax + Bx, bx = q(nd.qhi[0]) * Ax + Bx;
+        const float ay = q(nd.qlo[1]) * Ay + By, by = q(nd.qhi[1]) * Ay + By;
+        const float az = q(nd.qlo[2]) * Az + Bz, bz = q(nd.qhi[2]) * Az + Bz;
+        const float n = fmaxf(fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz)), 0.0f);
+        const float f = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)), t.t_best);
+        return (n <= f) & (nd.child[k] != WBVH_DONE) ? n : INFINITY;
+    };
+    float t0 = child_t(0), t1 = child_t(1), t2 = child_t(2), t3 = child_t(3);
+    int32_t c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+    wbvh_cswap(t0, c0, t1, c1);
+    wbvh_cswap(t2, c2, t3, c3);
+    wbvh_cswap(t0, c0, t2, c2);
+    wbvh_cswap(t1, c1, t3, c3);
+    wbvh_cswap(t1, c1, t2, c2);
+    if (t3 != INFINITY) stack[(t.sp++) * BLOCK] = c3;
+    if (t2 != INFINITY) stack[(t.sp++) * BLOCK] = c2;
+    if (t1 != INFINITY) stack[(t.sp++) * BLOCK] = c1;
+    t.node = t0 != INFINITY ? c0 : wbvh_pop(t, stack);
+}
+
+// One round: descend through inner nodes until the lane holds a leaf (or is
+// done), lanes waiting for the wave's slowest; then test the leaf.  With
+// NRT_SPECULATIVE (Aila & Laine) a lane that meets a leaf parks it and keeps
+// descending until every lane of the wave has a leaf.
+template <typename R, bool WIDE>
+__device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                                int32_t* stack) {
+#if NRT_SPECULATIVE
+    while (true) {
+        if (ts.node < 0 && ts.node != WBVH_DONE && ts.leaf == WBVH_NO_LEAF) {  // park a leaf
+            ts.leaf = ts.node;
+            ts.node = wbvh_pop(ts, stack);
+        }
+        const bool inner = ts.node >= 0;
+        if (!__any(inner)) break;                                         // nobody can descend
+        if (__all(ts.leaf != WBVH_NO_LEAF || ts.node == WBVH_DONE)) break;  // every lane has a leaf (or is done)
+        if (inner) {
+            if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
+            else wbvh2_visit(ts, sc, stack);
+        }
+    }
+    if (ts.leaf != WBVH_NO_LEAF) {
+        wbvh_leaf(ts, sc, ray, ts.leaf);
+        ts.leaf = WBVH_NO_LEAF;
+    }
+#else
+    while (ts.node >= 0) {
+        if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
+        else wbvh2_visit(ts, sc, stack);
+    }
+    if (ts.node == WBVH_DONE) return;
+    wbvh_leaf(ts, sc, ray, ts.node);
+    ts.node = wbvh_pop(ts, stack);
+#endif
+}
+
+template <typename R>
+__device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                           int32_t* stack) {
+    wbvh_round_impl<R, false>(ts, sc, ray, stack);
+}
+template <typename R>
+__device__ __forceinline__ void wbvh4_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                            int32_t* stack) {
+    wbvh_round_impl<R, true>(ts, sc, ray, stack);
+}
+
+// Root and round of the tree the scene carries (4-wide when its stack bound fits).
+template <typename R>
+__device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
+    return sc.wbvh4 ? sc.wbvh4_root : sc.wbvh_root;
+}
+template <typename R>
+__device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack) {
+    if (sc.wbvh4) wbvh4_round(ts, sc, ray, stack);
+    else wbvh_round(ts, sc, ray, stack);
 }
 
 template <typename R, int MAXD>
@@ -736,8 +842,8 @@ __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const R
                                                 int32_t* stack) {
     static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
     WbvhTrav ts;
-    wbvh_begin(ts, sc.wbvh_root, ray);
-    while (ts.node != WBVH_DONE) wbvh_round(ts, sc, ray, stack);
+    wbvh_begin(ts, wbvh_root(sc), ray);
+    while (ts.busy()) wbvh_step(ts, sc, ray, stack);
     hm.t = ts.t_best;
     hm.prim = (uint32_t)ts.best;
     hm.depth = 0;
@@ -1272,24 +1378,24 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // shows at least p.wave_wait lanes finished, then only those lanes shade and
         // start their next segment (active-ray compaction within the wave).
         static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
-        WbvhTrav ts;
+        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         bool active = camera_ray();
         auto begin = [&]() {
-            if (b < p.max_bounces) wbvh_begin(ts, gsc.wbvh_root, ray);
-            else ts.node = WBVH_DONE;  // depth cap: shaded as black without a query (Q6)
+            // depth cap: no query, the lane waits to be shaded as black (Q6)
+            wbvh_begin(ts, b < p.max_bounces ? wbvh_root(gsc) : WBVH_DONE, ray);
         };
         if (active) begin();
         const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
         while (true) {
             const unsigned long long t0 = stamp();
             while (true) {
-                const bool going = active && ts.node != WBVH_DONE;
+                const bool going = active && ts.busy();
                 if (__ballot(going) == 0ull) break;
-                if ((uint32_t)__popcll(__ballot(active && ts.node == WBVH_DONE)) >= wait_min) break;
-                if (going) wbvh_round(ts, gsc, ray, stack);
+                if ((uint32_t)__popcll(__ballot(active && !ts.busy())) >= wait_min) break;
+                if (going) wbvh_step(ts, gsc, ray, stack);
             }
             const unsigned long long t1 = stamp();
-            if (active && ts.node == WBVH_DONE) {
+            if (active && !ts.busy()) {
                 HitMin<R, MAXD> hm;
                 hm.t = ts.t_best;
                 hm.prim = (uint32_t)ts.best;

@@ -4,6 +4,7 @@
 
 #include "launch.hpp"
 
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -54,6 +55,14 @@ int gpu_device_count() {
     return n;
 }
 
+// 4-wide world BVH when the scene has one (its stack bound fits); NRT_WBVH4=0
+// keeps the binary tree (diagnostic A/B knob).
+static bool use_wbvh4(const FlatScene& fs) {
+    if (fs.wbvh.nodes4.empty()) return false;
+    const char* e = std::getenv("NRT_WBVH4");
+    return !(e && e[0] == '0');
+}
+
 DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
     check(hipSetDevice(device), "hipSetDevice");
     auto* ds = new DeviceScene();
@@ -78,6 +87,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* wpr = (DPrimWorld<float>*)track(upload(f32.wprims, "wprims"), f32.wprims.size() * sizeof(DPrimWorld<float>));
         auto* wrn = (uint32_t*)track(upload(fs.wruns, "wruns"), fs.wruns.size() * sizeof(uint32_t));
         auto* wbn = (DBvhNode*)track(upload(fs.wbvh.nodes, "wbvh"), fs.wbvh.nodes.size() * sizeof(DBvhNode));
+        auto* wb4 = (DBvh4Node*)track(upload(fs.wbvh.nodes4, "wbvh4"), fs.wbvh.nodes4.size() * sizeof(DBvh4Node));
         auto* wbp = (DPrimWorld<float>*)track(upload(f32.wbvh_prims, "wbvh_prims"),
                                               f32.wbvh_prims.size() * sizeof(DPrimWorld<float>));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
@@ -87,13 +97,15 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         // list-collapsed array with composed instance transforms.
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0, nullptr, 0, 0, nullptr, WBVH_DONE, 0};
+                                     nullptr, 0, nullptr, 0, 0, nullptr, nullptr, WBVH_DONE, WBVH_DONE, 0};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
-                                    (uint32_t)fs.wruns.size(), fs.wflags, wbn, fs.wbvh.root, (uint32_t)fs.wbvh.nodes.size()};
+                                    (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
+                                    fs.wbvh.root4, fs.wbvh.root,
+                                    (uint32_t)fs.wbvh.nodes.size()};
         ds->wbvh_ok = fs.wbvh_ok;
         ds->wbvh_prims = wbp;
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();

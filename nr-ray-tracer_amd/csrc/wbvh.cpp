@@ -1,13 +1,15 @@
 // Binned-SAH build of the f32 kernel's world BVH (wbvh.hpp).
 //
 // Standard top-down binned SAH (16 bins per axis, all three axes), traversal
-// cost 1, primitive cost 1, leaves of at most WBVH_LEAF_MAX primitives.  The
+// cost 1, per-primitive intersection costs from the caller, leaves of at most
+// WBVH_LEAF_MAX primitives.  The
 // tree is only an acceleration structure of the fast kernel: which primitive
 // is hit does not depend on it (closest hit, f32 statistical parity).
 #include "wbvh.hpp"
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 #include <stdexcept>
 
@@ -35,6 +37,7 @@ struct Item {
     Box box;
     double c[3];
     uint32_t index;
+    float cost;
 };
 
 struct Builder {
@@ -82,30 +85,37 @@ struct Builder {
             if (!(ext > 0.0)) continue;
             Box bin_box[BINS];
             size_t bin_n[BINS] = {};
+            double bin_c[BINS] = {};
             const double scale = BINS / ext;
             for (size_t i = b; i < e; ++i) {
                 int k = (int)((items[i].c[a] - cb.lo[a]) * scale);
                 k = std::min(std::max(k, 0), BINS - 1);
                 bin_box[k].grow(items[i].box);
                 ++bin_n[k];
+                bin_c[k] += items[i].cost;
             }
-            double right_area[BINS];
+            double right_area[BINS], right_c[BINS];
             size_t right_n[BINS];
             Box acc;
             size_t cnt = 0;
+            double csum = 0;
             for (int k = BINS - 1; k > 0; --k) {
                 acc.grow(bin_box[k]);
                 cnt += bin_n[k];
+                csum += bin_c[k];
                 right_area[k] = acc.area();
                 right_n[k] = cnt;
+                right_c[k] = csum;
             }
             acc = Box();
             cnt = 0;
+            csum = 0;
             for (int k = 0; k < BINS - 1; ++k) {  // split between bin k and k + 1
                 acc.grow(bin_box[k]);
                 cnt += bin_n[k];
+                csum += bin_c[k];
                 if (cnt == 0 || right_n[k + 1] == 0) continue;
-                const double cost = acc.area() * (double)cnt + right_area[k + 1] * (double)right_n[k + 1];
+                const double cost = acc.area() * csum + right_area[k + 1] * right_c[k + 1];
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = a;
@@ -113,7 +123,8 @@ struct Builder {
                 }
             }
         }
-        const double leaf_cost = (double)n;
+        double leaf_cost = 0;
+        for (size_t i = b; i < e; ++i) leaf_cost += items[i].cost;
         const double split_cost = 1.0 + best_cost / std::max(all.area(), 1e-300);
         size_t mid;
         if (best_axis < 0) {  // all centroids coincide: split by count
@@ -147,9 +158,81 @@ struct Builder {
     }
 };
 
+// Collapse the binary tree into 4-wide nodes: a 4-node's children are the
+// binary node's children with inner ones opened (largest box first) until four.
+struct Collapse {
+    const std::vector<DBvhNode>& n2;
+    std::vector<DBvh4Node>& n4;
+    struct Slot {
+        int32_t ref;
+        float lo[3], hi[3];
+    };
+    static float area(const Slot& c) {
+        const float x = c.hi[0] - c.lo[0], y = c.hi[1] - c.lo[1], z = c.hi[2] - c.lo[2];
+        return x * y + y * z + z * x;
+    }
+    int32_t build(int32_t ref) {  // ref: an inner binary node
+        std::vector<Slot> kids;
+        auto open = [&](int32_t r) {
+            const DBvhNode& b = n2[r];
+            Slot a{b.c0, {b.lo0[0], b.lo0[1], b.lo0[2]}, {b.hi0[0], b.hi0[1], b.hi0[2]}};
+            Slot c{b.c1, {b.lo1[0], b.lo1[1], b.lo1[2]}, {b.hi1[0], b.hi1[1], b.hi1[2]}};
+            kids.push_back(a);
+            kids.push_back(c);
+        };
+        open(ref);
+        while (kids.size() < 4) {
+            int best = -1;
+            for (int k = 0; k < (int)kids.size(); ++k)
+                if (kids[k].ref >= 0 && (best < 0 || area(kids[k]) > area(kids[best]))) best = k;
+            if (best < 0) break;
+            const int32_t r = kids[best].ref;
+            kids.erase(kids.begin() + best);
+            open(r);
+        }
+        const int32_t idx = (int32_t)n4.size();
+        n4.emplace_back();
+        int32_t child[4];
+        for (int k = 0; k < 4; ++k)
+            child[k] = k < (int)kids.size() ? (kids[k].ref >= 0 ? build(kids[k].ref) : kids[k].ref) : WBVH_DONE;
+        DBvh4Node& nd = n4[idx];
+        std::memset(&nd, 0, sizeof nd);
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (const Slot& k : kids) { lo = std::min(lo, k.lo[a]); hi = std::max(hi, k.hi[a]); }
+            nd.org[a] = lo;
+            // smallest power-of-two step with 255 steps covering the extent, then outward rounding
+            int e = hi > lo ? (int)std::ceil(std::log2(((double)hi - (double)lo) / 255.0)) : -126;
+            for (;; ++e) {
+                e = std::max(-126, std::min(127, e));
+                const float step = std::ldexp(1.0f, e);
+                bool ok = true;
+                uint32_t qlo = 0, qhi = 0;
+                for (size_t k = 0; k < kids.size() && ok; ++k) {
+                    double ql = std::floor(((double)kids[k].lo[a] - lo) / step), qh = std::ceil(((double)kids[k].hi[a] - lo) / step);
+                    ql = std::max(0.0, ql);
+                    while (ql > 0 && std::fma((float)ql, step, lo) > kids[k].lo[a]) ql -= 1;
+                    while (qh <= 255 && std::fma((float)qh, step, lo) < kids[k].hi[a]) qh += 1;
+                    if (qh > 255) { ok = false; break; }
+                    qlo |= (uint32_t)ql << (8 * k);
+                    qhi |= (uint32_t)qh << (8 * k);
+                }
+                if (!ok && e < 127) continue;
+                for (size_t k = kids.size(); k < 4; ++k) qlo |= 255u << (8 * k);  // empty slots (also ref-checked)
+                nd.qlo[a] = qlo;
+                nd.qhi[a] = qhi;
+                nd.exps |= (uint32_t)(e + 127) << (8 * a);
+                break;
+            }
+        }
+        for (int k = 0; k < 4; ++k) nd.child[k] = child[k];
+        return idx;
+    }
+};
+
 }  // namespace
 
-WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds) {
+WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const std::vector<float>& cost) {
     Builder bld;
     bld.items.resize(bounds.size());
     double scale = 0.0;
@@ -163,10 +246,33 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds) {
             if (std::isfinite(it.box.hi[k])) scale = std::max(scale, std::fabs(it.box.hi[k]));
         }
         it.index = (uint32_t)i;
+        it.cost = i < cost.size() ? cost[i] : 1.0f;
     }
     bld.pad = 1e-6 * std::max(scale, 1e-30);  // flat (axis-plane) primitives keep a volume
     if (!bounds.empty()) bld.out.root = bld.build(0, bld.items.size(), 0);
     if (bld.out.depth > WBVH_STACK) throw std::runtime_error("world BVH deeper than the kernel's stack");
+    if (bld.out.root >= 0) {
+        Collapse c{bld.out.nodes, bld.out.nodes4};
+        bld.out.root4 = c.build(bld.out.root);
+        // nearest-first pushes all but one hit child: bound the stack along every path
+        std::vector<uint32_t> need(bld.out.nodes4.size(), 0);
+        for (size_t i = bld.out.nodes4.size(); i-- > 0;) {  // children have larger indices
+            const DBvh4Node& nd = bld.out.nodes4[i];
+            uint32_t kids = 0, deepest = 0;
+            for (int k = 0; k < 4; ++k) {
+                if (nd.child[k] == WBVH_DONE) continue;
+                ++kids;
+                if (nd.child[k] >= 0) deepest = std::max(deepest, need[nd.child[k]]);
+            }
+            need[i] = (kids ? kids - 1 : 0) + deepest;
+        }
+        if (need[bld.out.root4] > WBVH_STACK) {  // too deep for 4-wide traversal: binary only
+            bld.out.nodes4.clear();
+            bld.out.root4 = WBVH_DONE;
+        }
+    } else {
+        bld.out.root4 = bld.out.root;  // a single leaf (or empty)
+    }
     return std::move(bld.out);
 }
 

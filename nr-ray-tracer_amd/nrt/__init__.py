@@ -20,7 +20,8 @@ from typing import Callable, Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnrt.so")
+# NRT_LIB: an experiment build of the same library (make OUT=... EXTRA=...); default the in-tree one
+LIB_PATH = os.environ.get("NRT_LIB") or os.path.join(_HERE, "libnrt.so")
 
 PRECISION = {"f64": 0, "f32": 1}
 RNG = {"chacha8": 0, "philox": 1}
