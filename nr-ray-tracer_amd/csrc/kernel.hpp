@@ -332,12 +332,19 @@ template <typename R> __device__ __forceinline__ V<R> unit_disk_inverse(uint32_t
 template <typename R>
 struct Ray {
     V<R> o, d;
-    V<R> inv;  // 1/d (fast variant only)
+    V<R> inv;  // 1/d for the slab tests
     R time;
 };
 
+// Both kernels multiply by 1/d in the slab test.  In the exact kernel 1/d is the
+// IEEE quotient (3 divisions per ray instead of 6 per box): (b - o) * (1/d)
+// differs from the reference's (b - o) / d by at most an ulp, while every box
+// carries the reference's 1e-4 padding, so no primitive the reference would
+// test is culled (or vice versa) outside measure-zero grazing cases; the
+// d = +-0 cases give the same +-inf / NaN slab ends as the division.
 template <typename R, bool EXACT> __device__ __forceinline__ void prep_ray(Ray<R>& r) {
-    if constexpr (!EXACT) r.inv = mk(fast_rcp(r.d.x), fast_rcp(r.d.y), fast_rcp(r.d.z));
+    if constexpr (EXACT) r.inv = mk(R(1) / r.d.x, R(1) / r.d.y, R(1) / r.d.z);
+    else r.inv = mk(fast_rcp(r.d.x), fast_rcp(r.d.y), fast_rcp(r.d.z));
 }
 
 // AABB::hit (aabb.rs:110-132) with range (0.001, t_max); t_max narrows during
@@ -347,18 +354,11 @@ template <typename R, bool EXACT>
 __device__ __forceinline__ bool box_hit(const R* bmin, const R* bmax, const Ray<R>& r, R t_max) {
     R lo = R(0.001), hi = t_max;
     const R* o = &r.o.x;
-    const R* d = &r.d.x;
     const R* iv = &r.inv.x;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        R a, b;
-        if constexpr (EXACT) {
-            a = (bmin[k] - o[k]) / d[k];
-            b = (bmax[k] - o[k]) / d[k];
-        } else {
-            a = (bmin[k] - o[k]) * iv[k];
-            b = (bmax[k] - o[k]) * iv[k];
-        }
+        const R a = (bmin[k] - o[k]) * iv[k];  // reference: (bmin - o) / d (see prep_ray)
+        const R b = (bmax[k] - o[k]) * iv[k];
         const bool lt = a < b;
         lo = fmax(lo, lt ? a : b);
         hi = fmin(hi, lt ? b : a);
@@ -764,7 +764,7 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
         const float az = q(nd.qlo[2]) * Az + Bz, bz = q(nd.qhi[2]) * Az + Bz;
         const float n = fmaxf(fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz)), 0.0f);
         const float f = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)), t.t_best);
-        return (n <= f) & (nd.child[k] != WBVH_DONE) ? n : INFINITY;
+        return ((n <= f) & (nd.child[k] != WBVH_DONE)) ? n : INFINITY;
     };
     float t0 = child_t(0), t1 = child_t(1), t2 = child_t(2), t3 = child_t(3);
     int32_t c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
