@@ -34,7 +34,7 @@ enum : uint32_t { PRIM_SPHERE = 0, PRIM_QUAD = 1, PRIM_TRIANGLE = 2, PRIM_BOX = 
 // (box headers: kind | face map << 3), runs = kind | count << 3.  World-list
 // only: quads whose plane normal is a coordinate axis (PRIM_QUAD_X + axis).
 constexpr uint32_t WKIND_BITS = 3, WKIND_MASK = 7;
-enum : uint32_t { PRIM_QUAD_X = 4, PRIM_QUAD_Y = 5, PRIM_QUAD_Z = 6 };
+enum : uint32_t { PRIM_QUAD_X = 4, PRIM_QUAD_Y = 5, PRIM_QUAD_Z = 6, PRIM_ABOX = 7 };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2 };
@@ -110,6 +110,13 @@ struct alignas(16) DPrimWorld {
 // quads that follow the header lies on plane x'_axis = side.  The quads keep
 // their own records (uv, normals, material) for the hit record.
 constexpr uint32_t BOX_ENTRIES = 7;
+// PRIM_ABOX (world list): axis quads that each cover a whole face of one axis-
+// aligned box (a "room": the Cornell walls) as one slab test; header N = lo,
+// AB[0..2] = hi, meta = PRIM_ABOX | face slots << 3 (3 bits per (axis, side),
+// 7 = no quad) | present-face mask << ABOX_PRESENT_SHIFT; then six slots
+// (present faces' quad records).  A ray hits the entry face if it is present
+// and t >= t_min, otherwise the exit face if present (the box is convex).
+constexpr uint32_t ABOX_PRESENT_SHIFT = 21;
 constexpr uint32_t WFLAG_AXIS_QUADS = 1;
 // Consecutive units of one kind form a run (kind | count << 2; a box unit is
 // BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised

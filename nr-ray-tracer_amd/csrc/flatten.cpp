@@ -1,7 +1,9 @@
 // Scene graph -> threaded BVH arrays (device_scene.hpp).
 #include "flatten.hpp"
 
+#include <climits>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <algorithm>
 #include <array>
@@ -408,6 +410,85 @@ struct Flattener {
         w.meta = (PRIM_QUAD_X + (uint32_t)a) | (w.meta & ~WKIND_MASK);
     }
 
+    // Axis quads that each cover a whole face of the bounding box of all axis
+    // quads (e.g. the Cornell room's walls) -> one PRIM_ABOX unit (device_scene.hpp).
+    void fuse_room(std::vector<std::vector<DPrimWorld<double>>>& units, std::vector<uint32_t>& kind,
+                   std::vector<size_t>& src) {
+        std::vector<size_t> aq;
+        for (size_t u = 0; u < units.size(); ++u)
+            if (kind[u] >= PRIM_QUAD_X && kind[u] <= PRIM_QUAD_Z) aq.push_back(u);
+        if (aq.size() < 2) return;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, scale = 0;
+        auto corners = [&](size_t u, V3a c[4]) {
+            const auto& g = wgeom[src[u]];
+            for (int k = 0; k < 4; ++k)
+                for (int r = 0; r < 3; ++r) c[k][r] = g[0][r] + ((k & 1) ? g[1][r] : 0.0) + ((k & 2) ? g[2][r] : 0.0);
+        };
+        for (size_t u : aq) {
+            V3a c[4];
+            corners(u, c);
+            for (auto& x : c)
+                for (int r = 0; r < 3; ++r) {
+                    lo[r] = std::min(lo[r], x[r]);
+                    hi[r] = std::max(hi[r], x[r]);
+                    scale = std::max(scale, std::fabs(x[r]));
+                }
+        }
+        const double tol = 1e-9 * std::max(scale, 1e-300);
+        long face[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};
+        int nfaces = 0;
+        for (size_t u : aq) {
+            const int a = (int)(kind[u] - PRIM_QUAD_X), a1 = (a + 1) % 3, a2 = (a + 2) % 3;
+            V3a c[4];
+            corners(u, c);
+            const double plane = c[0][a];
+            const int side = std::fabs(plane - lo[a]) <= tol ? 0 : (std::fabs(plane - hi[a]) <= tol ? 1 : -1);
+            if (side < 0 || face[a][side] >= 0 || !(hi[a1] > lo[a1]) || !(hi[a2] > lo[a2])) continue;
+            int seen = 0;  // the four corners must be the face's four corners
+            for (auto& x : c) {
+                const int b1 = std::fabs(x[a1] - lo[a1]) <= tol ? 0 : (std::fabs(x[a1] - hi[a1]) <= tol ? 1 : -1);
+                const int b2 = std::fabs(x[a2] - lo[a2]) <= tol ? 0 : (std::fabs(x[a2] - hi[a2]) <= tol ? 1 : -1);
+                if (b1 < 0 || b2 < 0 || std::fabs(x[a] - plane) > tol) { seen = -1; break; }
+                seen |= 1 << (b1 + 2 * b2);
+            }
+            if (seen != 15) continue;
+            face[a][side] = (long)u;
+            ++nfaces;
+        }
+        if (nfaces < 2) return;
+        std::vector<DPrimWorld<double>> unit(1 + 6);
+        DPrimWorld<double>& h = unit[0];
+        h = DPrimWorld<double>{};
+        for (int r = 0; r < 3; ++r) { h.N[r] = lo[r]; h.AB[r] = hi[r]; }
+        uint32_t map = 0, present = 0;
+        std::vector<bool> dead(units.size(), false);
+        for (int a = 0; a < 3; ++a)
+            for (int sd = 0; sd < 2; ++sd) {
+                const int slot = 2 * a + sd;
+                if (face[a][sd] >= 0) {
+                    unit[1 + slot] = units[face[a][sd]][0];
+                    map |= (uint32_t)slot << (3 * slot);
+                    present |= 1u << slot;
+                    dead[face[a][sd]] = true;
+                } else {
+                    unit[1 + slot] = DPrimWorld<double>{};  // absent face: never referenced
+                    map |= 7u << (3 * slot);
+                }
+            }
+        h.meta = PRIM_ABOX | (map << WKIND_BITS) | (present << ABOX_PRESENT_SHIFT);
+        std::vector<std::vector<DPrimWorld<double>>> nu;
+        std::vector<uint32_t> nk;
+        std::vector<size_t> ns;
+        for (size_t u = 0; u < units.size(); ++u)
+            if (!dead[u]) { nu.push_back(std::move(units[u])); nk.push_back(kind[u]); ns.push_back(src[u]); }
+        nu.push_back(std::move(unit));
+        nk.push_back(PRIM_ABOX);
+        ns.push_back(SIZE_MAX);
+        units.swap(nu);
+        kind.swap(nk);
+        src.swap(ns);
+    }
+
     // Six consecutive quads closing a parallelepiped -> PRIM_BOX header (device_scene.hpp).
     bool fuse_box(size_t i, DPrimWorld<double>& hdr) const {
         std::vector<V3a> pts;
@@ -691,6 +772,7 @@ struct Flattener {
         // between coincident surfaces (the reference's order is kept within a kind).
         std::vector<std::vector<DPrimWorld<double>>> units;
         std::vector<uint32_t> unit_kind;
+        std::vector<size_t> unit_src;  // wprims index of a single-primitive unit
         for (size_t i = 0; i < out.wprims.size();) {
             DPrimWorld<double> hdr;
             if (i + 6 <= out.wprims.size() && fuse_box(i, hdr)) {
@@ -698,16 +780,19 @@ struct Flattener {
                 u.insert(u.end(), out.wprims.begin() + i, out.wprims.begin() + i + 6);
                 units.push_back(std::move(u));
                 unit_kind.push_back(PRIM_BOX);
+                unit_src.push_back(SIZE_MAX);
                 i += 6;
             } else {
                 DPrimWorld<double> w = out.wprims[i];
                 if ((w.meta & WKIND_MASK) == PRIM_QUAD) axis_quad(w);
                 units.push_back({w});
                 unit_kind.push_back(w.meta & WKIND_MASK);
+                unit_src.push_back(i);
                 ++i;
             }
         }
-        static const int rank[7] = {5, 3, 4, 6, 0, 1, 2};  // X, Y, Z quads, quads, triangles, spheres, boxes
+        fuse_room(units, unit_kind, unit_src);
+        static const int rank[8] = {5, 3, 4, 6, 0, 1, 2, 7};  // X, Y, Z quads, quads, triangles, spheres, boxes, rooms
         std::vector<size_t> order(units.size());
         for (size_t k = 0; k < order.size(); ++k) order[k] = k;
         std::stable_sort(order.begin(), order.end(),
@@ -722,7 +807,7 @@ struct Flattener {
         out.world_units = kinds.size();
         const uint32_t one = 1u << WKIND_BITS;
         for (uint32_t kind : kinds) {
-            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;
+            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;  // axis quads and rooms use 1/d
             if (!out.wruns.empty() && (out.wruns.back() & WKIND_MASK) == kind && (out.wruns.back() >> WKIND_BITS) < (1u << 28))
                 out.wruns.back() += one;
             else

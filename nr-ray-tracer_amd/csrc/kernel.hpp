@@ -577,6 +577,27 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
         if (kind == PRIM_QUAD_X) { axis_quad_run<0>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
         if (kind == PRIM_QUAD_Y) { axis_quad_run<1>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
         if (kind == PRIM_QUAD_Z) { axis_quad_run<2>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
+        if (kind == PRIM_ABOX) {  // room: axis-aligned box whose present faces are quads
+            for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
+                const ConstPrimWorld<float> q = wp + k;
+                const uint32_t present = q->meta >> ABOX_PRESENT_SHIFT;
+                const float lx = q->N[0] * inv[0] - oinv[0], hx = q->AB[0] * inv[0] - oinv[0];
+                const float ly = q->N[1] * inv[1] - oinv[1], hy = q->AB[1] * inv[1] - oinv[1];
+                const float lz = q->N[2] * inv[2] - oinv[2], hz = q->AB[2] * inv[2] - oinv[2];
+                const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+                const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+                const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+                // face slots 2*axis + side: entry on the low plane when d > 0, exit on the high one
+                const uint32_t e = tn == nx ? (lx < hx ? 0u : 1u) : (tn == ny ? (ly < hy ? 2u : 3u) : (lz < hz ? 4u : 5u));
+                const uint32_t x = tf == fx ? (lx < hx ? 1u : 0u) : (tf == fy ? (ly < hy ? 3u : 2u) : (lz < hz ? 5u : 4u));
+                const bool use_entry = (tn >= 0.001f) & (((present >> e) & 1u) != 0u);
+                const float t = use_entry ? tn : tf;
+                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) & (use_entry | (((present >> x) & 1u) != 0u));
+                t_best = ok ? t : t_best;
+                best = ok ? (int32_t)k : best;
+            }
+            continue;
+        }
         if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
             for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
                 const ConstPrimWorld<float> q = wp + k;
@@ -985,6 +1006,20 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
             if (d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
         }
         prim += 1 + ((q.meta >> (WKIND_BITS + 3 * slot)) & 7u);
+        q = load16(sc.wprims + prim);
+    } else if ((q.meta & WKIND_MASK) == PRIM_ABOX) {
+        // which present face: the hit point's nearest face plane
+        const uint32_t present = q.meta >> ABOX_PRESENT_SHIFT;
+        uint32_t slot = 0;
+        R dmin = R(INFINITY);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const R c = (&pw.x)[a];
+            const R d0 = fabs(c - q.N[a]), d1 = fabs(c - q.AB[a]);
+            if (((present >> (2 * a)) & 1u) && d0 < dmin) { dmin = d0; slot = 2 * a; }
+            if (((present >> (2 * a + 1)) & 1u) && d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
+        }
+        prim += 1 + slot;
         q = load16(sc.wprims + prim);
     }
     const uint32_t kind = q.meta & WKIND_MASK;
