@@ -594,7 +594,7 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
                 const float t = use_entry ? tn : tf;
                 const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) & (use_entry | (((present >> x) & 1u) != 0u));
                 t_best = ok ? t : t_best;
-                best = ok ? (int32_t)k : best;
+                best = ok ? (int32_t)(k + 1 + (use_entry ? e : x)) : best;  // the face quad's record
             }
             continue;
         }
@@ -612,10 +612,16 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
                 const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
                 const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                 // entry face unless it lies before t_min (origin on or inside the box): then the exit face
-                const float t = tn >= 0.001f ? tn : tf;
+                const bool entry = tn >= 0.001f;
+                const float t = entry ? tn : tf;
                 const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+                // face slot 2*axis + side (side 0 = local plane x' = 0), then the quad that lies there
+                const uint32_t slot =
+                    entry ? (tn == fminf(ax, bx) ? (ax < bx ? 0u : 1u) : (tn == fminf(ay, by) ? (ay < by ? 2u : 3u) : (az < bz ? 4u : 5u)))
+                          : (tf == fmaxf(ax, bx) ? (ax < bx ? 1u : 0u) : (tf == fmaxf(ay, by) ? (ay < by ? 3u : 2u) : (az < bz ? 5u : 4u)));
+                const uint32_t face = (q->meta >> (WKIND_BITS + 3 * slot)) & 7u;
                 t_best = ok ? t : t_best;
-                best = ok ? (int32_t)k : best;
+                best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
             }
             continue;
         }
@@ -985,43 +991,15 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
 }
 
 // HitRecord of the winner (HitRecord::new_with_uv, hitable.rs:38-59).
-// World-space record (MAXD = 0; device_scene.hpp DPrimWorld): the
+// World-space record (MAXD <= 0; device_scene.hpp DPrimWorld): the
 // reference's front-face sign signum(d'.n) = signum(d.(M^T n)), shading normal
 // mapped out by the chain's rotations only.
 template <typename R, int MAXD>
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
-    uint32_t prim = hm.prim;
-    DPrimWorld<R> q = load16(sc.wprims + prim);
+    // hm.prim is always a primitive record: box and room hits name their face quad
+    const DPrimWorld<R> q = load16(sc.wprims + hm.prim);
     const V<R> pw = wray.o + hm.t * wray.d;
-    if ((q.meta & WKIND_MASK) == PRIM_BOX) {
-        // which face: the local coordinate of the hit point nearest a face plane
-        const R l[3] = {dot(ld3(q.N), pw) - q.D, dot(ld3(q.AB), pw) - q.AB[3], dot(ld3(q.AB + 4), pw) - q.AB[7]};
-        uint32_t slot = 0;
-        R dmin = R(INFINITY);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const R d0 = fabs(l[a]), d1 = fabs(l[a] - R(1));
-            if (d0 < dmin) { dmin = d0; slot = 2 * a; }
-            if (d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
-        }
-        prim += 1 + ((q.meta >> (WKIND_BITS + 3 * slot)) & 7u);
-        q = load16(sc.wprims + prim);
-    } else if ((q.meta & WKIND_MASK) == PRIM_ABOX) {
-        // which present face: the hit point's nearest face plane
-        const uint32_t present = q.meta >> ABOX_PRESENT_SHIFT;
-        uint32_t slot = 0;
-        R dmin = R(INFINITY);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const R c = (&pw.x)[a];
-            const R d0 = fabs(c - q.N[a]), d1 = fabs(c - q.AB[a]);
-            if (((present >> (2 * a)) & 1u) && d0 < dmin) { dmin = d0; slot = 2 * a; }
-            if (((present >> (2 * a + 1)) & 1u) && d1 < dmin) { dmin = d1; slot = 2 * a + 1; }
-        }
-        prim += 1 + slot;
-        q = load16(sc.wprims + prim);
-    }
     const uint32_t kind = q.meta & WKIND_MASK;
     Rec<R> h;
     h.p = pw;
