@@ -4,6 +4,15 @@
 // (render.rs:57-62), gamma 0.5 + to_rgb8 + write (render.rs:74-102).
 // Extra flags: --precision {f64,f32}, --rng {chacha8,philox}, --gpus N.
 // Output formats: .png (stored deflate), .ppm, .pfm (linear f32).
+//
+// `nrt-cli convert-stl <STL> [-o FILE] [-f] [-F toml|json]` — the reference's
+// `create convert-stl` (app/commands/create/convert_stl.rs:19-138): binary STL
+// -> one Group of Triangles, vertices read as (x, z, -y), k = 1 / max extent,
+// point = k (a - p_min), u = k (b - a), v = k (c - a), camera look_at
+// (k l/2, k h/2, 0), look_from = look_at + Z, white background, fov 50,
+// 50 bounces, spp 200, "# model bbox" header line.
+#include <array>
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -105,9 +114,105 @@ void write_png(FILE* f, uint32_t w, uint32_t h, const std::vector<uint8_t>& rgb)
     chunk(f, "IEND", {});
 }
 
+std::string shortest(double x) {  // Rust's f64 Display: shortest round-trip digits, "1.0" style
+    if (x == 0.0) return std::signbit(x) ? "-0.0" : "0.0";
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, x);
+    std::string t(buf, r.ptr);
+    if (t.find_first_of(".eEn") == std::string::npos) t += ".0";
+    return t;
+}
+
+int convert_stl(int argc, char** argv) {  // argv[1] == "convert-stl"
+    std::string input, output, format = "toml";
+    bool force = false;
+    for (int i = 2; i < argc; ++i) {
+        const std::string a = argv[i];
+        auto val = [&]() -> std::string {
+            if (i + 1 >= argc) die("missing value for " + a);
+            return argv[++i];
+        };
+        if (a == "-o" || a == "--output") output = val();
+        else if (a == "-f" || a == "--force-overwrite") force = true;
+        else if (a == "-F" || a == "--format") format = val();
+        else if (!a.empty() && a[0] == '-') die("unknown option " + a);
+        else input = a;
+    }
+    if (input.empty()) die("missing STL file");
+    if (format != "toml" && format != "json") die("--format must be toml or json");
+    FILE* in = fopen(input.c_str(), "rb");
+    if (!in) die("No such file or directory (os error 2)");
+    uint8_t header[80];
+    uint32_t count = 0;
+    if (fread(header, 1, 80, in) != 80 || fread(&count, 4, 1, in) != 1) die("failed to fill whole buffer");
+    using V = std::array<double, 3>;
+    std::vector<std::array<V, 3>> tris(count);
+    V lo{INFINITY, INFINITY, INFINITY}, hi{-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t t = 0; t < count; ++t) {
+        float f[12];
+        uint16_t attr;
+        if (fread(f, 4, 12, in) != 12 || fread(&attr, 2, 1, in) != 1) die("failed to fill whole buffer");
+        for (int k = 0; k < 3; ++k) {  // skip the normal (f[0..2]); DVec3::new(x, z, -y)
+            const V p{(double)f[3 + 3 * k], (double)f[5 + 3 * k], -(double)f[4 + 3 * k]};
+            tris[t][k] = p;
+            for (int r = 0; r < 3; ++r) { lo[r] = std::min(lo[r], p[r]); hi[r] = std::max(hi[r], p[r]); }
+        }
+    }
+    fclose(in);
+    const double l = hi[0] - lo[0], h = hi[1] - lo[1], w = hi[2] - lo[2];
+    const double k = 1.0 / std::max(std::max(l, w), h);
+    const V look_at{k * l / 2.0, k * h / 2.0, 0.0};
+    const V look_from{look_at[0], look_at[1], look_at[2] + 1.0};
+    auto vec = [](const V& v) { return "[" + shortest(v[0]) + ", " + shortest(v[1]) + ", " + shortest(v[2]) + "]"; };
+    std::string out;
+    char hdr[128];
+    snprintf(hdr, sizeof hdr, "# model bbox: l=%.4f h=%.4f w=%.4f\n", k * l, k * h, k * w);
+    out += hdr;
+    std::vector<std::array<V, 3>> puv;
+    for (auto& t : tris) {
+        V p, u, v;
+        for (int r = 0; r < 3; ++r) {
+            p[r] = k * (t[0][r] - lo[r]);
+            u[r] = k * (t[1][r] - t[0][r]);
+            v[r] = k * (t[2][r] - t[0][r]);
+        }
+        puv.push_back({p, u, v});
+    }
+    if (format == "toml") {
+        out += "[camera]\nbackground_color = [1.0, 1.0, 1.0]\nlook_at = " + vec(look_at) + "\nlook_from = " + vec(look_from) +
+               "\nfield_of_view = 50.0\nsamples_per_pixel = 200\nray_max_bounces = 50\n\n[[scene]]\n\n[scene.Group]\n";
+        for (auto& t : puv)
+            out += "\n[[scene.Group.objects]]\n\n[scene.Group.objects.Triangle]\npoint = " + vec(t[0]) + "\nu = " + vec(t[1]) +
+                   "\nv = " + vec(t[2]) + "\n";
+    } else {
+        out += "{\n  \"camera\": {\n    \"width\": null,\n    \"height\": null,\n    \"aspect_ratio\": null,\n"
+               "    \"background_color\": [1.0, 1.0, 1.0],\n    \"look_at\": " + vec(look_at) + ",\n    \"look_from\": " +
+               vec(look_from) + ",\n    \"view_up\": null,\n    \"focal_length\": null,\n    \"field_of_view\": 50.0,\n"
+               "    \"defocus_angle\": null,\n    \"focus_distance\": null,\n    \"samples_per_pixel\": 200,\n"
+               "    \"ray_max_bounces\": 50\n  },\n  \"scene\": [\n    {\n      \"Group\": {\n        \"objects\": [";
+        for (size_t i = 0; i < puv.size(); ++i)
+            out += std::string(i ? "," : "") + "\n          {\"Triangle\": {\"point\": " + vec(puv[i][0]) + ", \"u\": " +
+                   vec(puv[i][1]) + ", \"v\": " + vec(puv[i][2]) + "}}";
+        out += "\n        ]\n      }\n    }\n  ]\n}";
+    }
+    if (output.empty()) {
+        fwrite(out.data(), 1, out.size(), stdout);
+        return 0;
+    }
+    if (!force) {
+        if (FILE* e = fopen(output.c_str(), "rb")) { fclose(e); die("File exists (os error 17)"); }
+    }
+    FILE* o = fopen(output.c_str(), "wb");
+    if (!o) die("cannot open " + output);
+    fwrite(out.data(), 1, out.size(), o);
+    fclose(o);
+    return 0;
+}
+
 void usage() {
     fprintf(stderr,
-            "usage: nrt-cli render <SCENE> [-o FILE] [-f] [--gamma-value G] [-W W] [-H H] [--aspect-ratio R]\n"
+            "usage: nrt-cli convert-stl <STL> [-o FILE] [-f] [-F toml|json]\n"
+            "       nrt-cli render <SCENE> [-o FILE] [-f] [--gamma-value G] [-W W] [-H H] [--aspect-ratio R]\n"
             "       [--background-color X,Y,Z] [--look-at X,Y,Z] [--look-from X,Y,Z] [--view-up X,Y,Z]\n"
             "       [--focal-length F] [--field-of-view DEG] [--defocus-angle DEG] [--focus-distance D]\n"
             "       [--samples-per-pixel N] [--ray-max-bounces N] [-v]\n"
@@ -118,6 +223,7 @@ void usage() {
 }  // namespace
 
 int main(int argc, char** argv) {
+    if (argc >= 3 && std::string(argv[1]) == "convert-stl") return convert_stl(argc, argv);
     if (argc < 3 || std::string(argv[1]) != "render") usage();
     std::string scene, output = "out.png";
     bool force = false, verbose = false;
