@@ -64,6 +64,12 @@ def test_convert_stl_matches_reference_transform(fmt, tmp_path):
         np.testing.assert_allclose(tri["point"], p, rtol=0, atol=1e-15)
         np.testing.assert_allclose(tri["u"], u, rtol=0, atol=1e-15)
         np.testing.assert_allclose(tri["v"], v, rtol=0, atol=1e-15)
+    if fmt == "json":
+        # the reference writes the "# model bbox" line before the JSON body too (convert_stl.rs:128-135),
+        # so its JSON output does not parse as a scene -- same here
+        with pytest.raises(nrt.NrtError):
+            nrt.Scene.load(str(out))
+        return
     # loads through the library and the oracle's loader identically (camera + graph dump)
     from test_loader_parity import _norm, product_dump
     got, s = product_dump(str(out), dict(width=16, height=16, spp=1))
