@@ -562,12 +562,14 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     int32_t best = -1;
     // (d, o) pairs: N.d and N.o come out of one packed FMA chain
     const f32x2 dox = {ray.d.x, ray.o.x}, doy = {ray.d.y, ray.o.y}, doz = {ray.d.z, ray.o.z};
-    float inv[3], oinv[3];  // axis-aligned quads: 1/d and o/d
+    float inv[3], oinv[3];  // axis-aligned quads and rooms: 1/d and o/d
+    uint32_t entry_slot[3] = {0u, 2u, 4u};  // rooms: face slot 2*axis + side entered along each axis
     if (sc.wflags & WFLAG_AXIS_QUADS) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             inv[a] = __builtin_amdgcn_rcpf((&ray.d.x)[a]);
             oinv[a] = (&ray.o.x)[a] * inv[a];
+            entry_slot[a] = 2u * a + (inv[a] < 0.0f ? 1u : 0u);  // d > 0 enters at the low plane
         }
     }
     uint32_t k = 0;
@@ -587,12 +589,16 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
                 const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
                 const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
                 const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
-                // face slots 2*axis + side: entry on the low plane when d > 0, exit on the high one
-                const uint32_t e = tn == nx ? (lx < hx ? 0u : 1u) : (tn == ny ? (ly < hy ? 2u : 3u) : (lz < hz ? 4u : 5u));
-                const uint32_t x = tf == fx ? (lx < hx ? 1u : 0u) : (tf == fy ? (ly < hy ? 3u : 2u) : (lz < hz ? 5u : 4u));
-                const bool use_entry = (tn >= 0.001f) & (((present >> e) & 1u) != 0u);
+                // face slots 2*axis + side (branch-free selects): entry slots from the ray's
+                // direction signs, exit = the opposite side of the exit axis
+                uint32_t e = entry_slot[2], x = entry_slot[2] ^ 1u;
+                e = tn == ny ? entry_slot[1] : e;
+                e = tn == nx ? entry_slot[0] : e;
+                x = tf == fy ? entry_slot[1] ^ 1u : x;
+                x = tf == fx ? entry_slot[0] ^ 1u : x;
+                const bool use_entry = (tn >= 0.001f) & (__builtin_amdgcn_ubfe(present, e, 1) != 0u);
                 const float t = use_entry ? tn : tf;
-                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) & (use_entry | (((present >> x) & 1u) != 0u));
+                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) & (use_entry | (__builtin_amdgcn_ubfe(present, x, 1) != 0u));
                 t_best = ok ? t : t_best;
                 best = ok ? (int32_t)(k + 1 + (use_entry ? e : x)) : best;  // the face quad's record
             }
@@ -615,11 +621,16 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
                 const bool entry = tn >= 0.001f;
                 const float t = entry ? tn : tf;
                 const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
-                // face slot 2*axis + side (side 0 = local plane x' = 0), then the quad that lies there
-                const uint32_t slot =
-                    entry ? (tn == fminf(ax, bx) ? (ax < bx ? 0u : 1u) : (tn == fminf(ay, by) ? (ay < by ? 2u : 3u) : (az < bz ? 4u : 5u)))
-                          : (tf == fmaxf(ax, bx) ? (ax < bx ? 1u : 0u) : (tf == fmaxf(ay, by) ? (ay < by ? 3u : 2u) : (az < bz ? 5u : 4u)));
-                const uint32_t face = (q->meta >> (WKIND_BITS + 3 * slot)) & 7u;
+                // face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0),
+                // then the quad that lies there (3 bits per slot in meta)
+                const uint32_t sx = ix < 0.0f ? 1u : 0u, sy = iy < 0.0f ? 3u : 2u, sz = iz < 0.0f ? 5u : 4u;
+                uint32_t se = sz, sxit = sz ^ 1u;
+                se = tn == fminf(ay, by) ? sy : se;
+                se = tn == fminf(ax, bx) ? sx : se;
+                sxit = tf == fmaxf(ay, by) ? sy ^ 1u : sxit;
+                sxit = tf == fmaxf(ax, bx) ? sx ^ 1u : sxit;
+                const uint32_t slot = entry ? se : sxit;
+                const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
                 t_best = ok ? t : t_best;
                 best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
             }
