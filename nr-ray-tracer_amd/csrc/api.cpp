@@ -180,6 +180,19 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) p.wave_wait = (uint32_t)v;
     }
+    // Philox lanes per pixel: 4 keeps a GPU full down to 1/8 of a 1024^2 frame (the
+    // 8-GPU row share) and is fixed per frame, so any row partition sums each
+    // pixel's samples in the same order (bitwise-identical frames for every N).
+    // Tuning knob NRT_SPLIT: 1, 2, 4, 8.  ChaCha8 streams are sequential: always 1.
+    p.split = 1;
+    if (o && o->rng == NRT_RNG_PHILOX) {
+        const uint64_t spp = c.samples_per_pixel;
+        p.split = spp >= 4 ? 4u : (spp >= 2 ? 2u : 1u);
+        if (const char* e = std::getenv("NRT_SPLIT")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v == 1 || v == 2 || v == 4 || v == 8) p.split = (uint32_t)v;
+        }
+    }
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;

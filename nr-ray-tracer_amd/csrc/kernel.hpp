@@ -1226,7 +1226,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + stack_bytes);
 
-    const uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
+    // Philox mode may split a pixel's samples over p.split adjacent lanes (sample s on
+    // lane s mod split, its own counter), summed at the end in a fixed shuffle tree.
+    const uint32_t split = G::exact_stream ? 1u : p.split;
+    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t i = p.pixel_begin + tid / split, sub = tid % split;
     if (i >= p.pixel_end) return;
     const uint32_t x = i % p.width;
     const uint32_t row = i / p.width;
@@ -1245,20 +1249,21 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     const V<R> background = cam(6, p.background);
 
     double ax = 0.0, ay = 0.0, az = 0.0;
-    uint32_t s = 0, b = 0, cur = 0;  // samples started, bounces of this path, current sample
+    uint32_t s = sub, b = 0, cur = 0;  // next sample of this lane, bounces of this path, current sample
     bool bounced = false;
     Ray<R> ray;
     V<R> tp = mk(R(1), R(1), R(1));
     // Philox mode: the block this lane consumes next (exactly one per path segment,
     // computed by every shading lane at the same point: no divergent refills)
     uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if constexpr (!G::exact_stream) w = g.block(0u, 0u);
+    if constexpr (!G::exact_stream) w = g.block(sub, 0u);
 
     // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
     auto camera_ray = [&]() -> bool {
         if (s >= p.spp) return false;
         g.start_sample(s);
-        cur = s++;
+        cur = s;
+        s += split;
         R ox = R(0), oy = R(0);
         if constexpr (G::exact_stream) {
             if (p.spp > 1) {
@@ -1335,8 +1340,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         }
         const unsigned long long s1 = stamp();
         // Philox: this segment's block -- the scatter's (pixel, sample, bounce + 1), or, when
-        // the path ends here, the next sample's camera block (pixel, sample + 1, 0)
-        if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + 1, scatter ? b + 1 : 0u);
+        // the path ends here, the lane's next sample's camera block (pixel, sample + split, 0)
+        if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + split, scatter ? b + 1 : 0u);
         const unsigned long long s2 = stamp();
         if (scatter) {
             V<R> dir;
@@ -1377,7 +1382,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ++b;
                 term = false;
             } else if constexpr (!G::exact_stream) {
-                w = g.block(cur + 1, 0u);  // absorbed by a metal: the next sample's camera block
+                w = g.block(cur + split, 0u);  // absorbed by a metal: the next sample's camera block
             }
         }
         if (term) {
@@ -1473,6 +1478,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (c != 4) atomicAdd(&p.counters[c], prof[wave][c]);
             atomicAdd(&p.counters[4], 1ull);
         }
+    }
+    if constexpr (!G::exact_stream) {
+        for (uint32_t m = 1; m < split; m <<= 1) {  // fixed order: every lane ends with the same sum
+            ax += __shfl_xor(ax, (int)m);
+            ay += __shfl_xor(ay, (int)m);
+            az += __shfl_xor(az, (int)m);
+        }
+        if (sub != 0) return;
     }
     const double spp = (double)p.spp;
     float* o = p.out + 3ull * i;

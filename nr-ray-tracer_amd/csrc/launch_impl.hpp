@@ -12,7 +12,7 @@ constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 
 template <typename R, class G, int MAXD, bool EXACT>
 static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_t stream) {
-    const uint32_t n = p.pixel_end - p.pixel_begin;
+    const uint32_t n = (p.pixel_end - p.pixel_begin) * (G::exact_stream ? 1u : p.split);  // lanes
     const uint32_t blocks = (n + dev::BLOCK - 1) / dev::BLOCK;
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
                           (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);  // + BVH stack

@@ -22,6 +22,7 @@ struct RenderParams {
     float camf[7][3];
     uint32_t defocus;  // 0: defocus disk is zero (defocus_angle <= 0), disk draws only feed the origin
     uint32_t wave_wait;  // world-BVH mode: lanes that must finish traversal before a shading round
+    uint32_t split;      // Philox mode: lanes per pixel (power of two <= 64); 1 for ChaCha8
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;

@@ -79,6 +79,17 @@ def test_f64_chacha8_matches_oracle(scene, w, h, spp, bounces):
     assert np.max(rel) <= 1e-6, f"max rel err {np.max(rel):.3e}"
 
 
+def test_philox_row_interleave_is_bitwise_identical():
+    # split lanes per pixel are fixed per frame: any row partition sums samples in the same order
+    scene, w, h, spp = "scenes/cornell-box-scene.json", 32, 21, 16
+    s = load(scene, w, h, spp)
+    full = s.render(precision="f32", rng="philox")
+    for stride in (2, 8):
+        for off in range(stride):
+            part = s.render(precision="f32", rng="philox", row_offset=off, row_stride=stride)
+            np.testing.assert_array_equal(part, full[off::stride])
+
+
 def test_row_interleave_is_bitwise_identical():
     # RNG keyed by pixel index: any row partition gives the same pixels
     scene, w, h, spp = "scenes/cornell-box-scene.json", 32, 21, 4
