@@ -206,9 +206,10 @@ int nrt_image_to_rgb8(const float* rgb, size_t n_floats, float gamma, uint8_t* o
  * (ChaCha8: stream = pixel index; Philox: counter (pixel, sample, pair)). */
 int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out);
 
-/* Diagnostics: one render of the LDS-resident kernel with per-wave s_memtime
- * stamps; out[0..4] = {loop iterations, camera-ray cycles, trace cycles,
- * shading cycles, waves} summed over waves.  Slower than nrt_render; never timed. */
+/* Diagnostics: one render with per-wave s_memtime stamps; out[0..4] = {loop
+ * iterations, camera-ray cycles, trace cycles, shading cycles, waves} summed over
+ * waves, and with n >= 8 out[5..7] = the shading cycles split into {hit record +
+ * material, Philox block, scatter + accumulate}.  Slower than nrt_render; never timed. */
 int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
                             uint64_t* out, size_t n);
 
