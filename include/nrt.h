@@ -209,7 +209,9 @@ int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count
 /* Diagnostics: one render with per-wave s_memtime stamps; out[0..4] = {loop
  * iterations, camera-ray cycles, trace cycles, shading cycles, waves} summed over
  * waves, and with n >= 8 out[5..7] = the shading cycles split into {hit record +
- * material, Philox block, scatter + accumulate}.  Slower than nrt_render; never timed. */
+ * material, sample claim + Philox block, scatter / camera ray + accumulate}.  With
+ * rng = Philox, camera rays are part of shading and out[1] counts the lane-iterations
+ * that shaded a path instead.  Slower than nrt_render; never timed. */
 int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
                             uint64_t* out, size_t n);
 

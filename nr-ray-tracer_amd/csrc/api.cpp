@@ -156,7 +156,7 @@ int resolve_device(const nrt_render_opts* o) {
     return dev;
 }
 
-RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t rows) {
+RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t rows, const FlatScene& f) {
     if (c.width == 0 || c.height == 0) throw std::invalid_argument("image width and height must be > 0");
     if (c.width * c.height > 0xFFFFFFFFull) throw std::invalid_argument("image has more than 2^32 pixels");
     if (c.samples_per_pixel > 0xFFFFFFFFull || c.ray_max_bounces > 0xFFFFFFFFull)
@@ -180,23 +180,47 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) p.wave_wait = (uint32_t)v;
     }
-    // Philox lanes per pixel: 4 keeps a GPU full down to 1/8 of a 1024^2 frame (the
-    // 8-GPU row share) and is fixed per frame, so any row partition sums each
-    // pixel's samples in the same order (bitwise-identical frames for every N).
-    // Tuning knob NRT_SPLIT: 1, 2, 4, 8.  ChaCha8 streams are sequential: always 1.
-    p.split = 1;
-    if (o && o->rng == NRT_RNG_PHILOX) {
-        const uint64_t spp = c.samples_per_pixel;
-        p.split = spp >= 4 ? 4u : (spp >= 2 ? 2u : 1u);
-        if (const char* e = std::getenv("NRT_SPLIT")) {
-            const long v = std::strtol(e, nullptr, 10);
-            if (v == 1 || v == 2 || v == 4 || v == 8) p.split = (uint32_t)v;
-        }
-    }
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;
     p.max_bounces = (uint32_t)c.ray_max_bounces;
+    // Philox sample pool: pixels per wave, 0 = chosen per launch (render.hip); tuning
+    // knob NRT_WAVE_PIXELS (a power of two 1..128).  ChaCha8 streams are sequential:
+    // one lane per pixel.
+    p.wave_pixels = 1;
+    if (o && o->rng == NRT_RNG_PHILOX) {
+        p.wave_pixels = 0;
+        if (const char* e = std::getenv("NRT_WAVE_PIXELS")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v >= 1 && v <= 128 && (v & (v - 1)) == 0) p.wave_pixels = (uint32_t)v;
+        }
+        if (c.width > 0xFFFFu || c.height > 0xFFFFu)
+            throw std::invalid_argument("Philox mode: image width and height must be < 65536");
+        if ((uint64_t)128 * p.spp >= 0xFFFFFFFFull)
+            throw std::invalid_argument("samples_per_pixel too large for the Philox sample pool (< 2^25)");
+    }
+    // Radiance grid 2^-k: a sample's radiance is at most max(background, emission) x
+    // albedo^bounces; k keeps spp such values below 2^52, so the pixel sums are exact
+    // (order-free).  Albedo > 1 is counted over at most 8 bounces: past that the sums
+    // round like any f64 sum (still deterministic per lane order, no longer order-free).
+    {
+        double emit = 0.0, alb = 1.0;
+        for (int k = 0; k < 3; ++k) emit = std::fmax(emit, std::fabs(c.background_color[k]));
+        double texmax = 1.0;  // image texels are <= 1
+        for (const DTexture& t : f.textures)
+            if (t.kind == TEX_SOLID)
+                for (int k = 0; k < 3; ++k) texmax = std::fmax(texmax, std::fabs(t.color[k]));
+        for (const DMaterial& m : f.materials) {
+            if (m.kind == MAT_DIFFUSE_LIGHT) emit = std::fmax(emit, std::fmax(1.0, std::fabs(m.param)) * texmax);
+        }
+        alb = texmax;
+        double lg = std::log2(std::fmax(emit, 1e-300)) + std::log2((double)p.spp) +
+                    std::log2(alb) * (double)std::min<uint32_t>(p.max_bounces, 8u);
+        int k = 50 - (int)std::ceil(std::fmax(lg, -100.0));
+        k = std::max(-900, std::min(k, 900));
+        p.acc_scale = std::ldexp(1.0, k);
+        p.acc_unscale = std::ldexp(1.0, -k);
+    }
     p.row_offset = o ? o->row_offset : 0;
     p.row_stride = (o && o->row_stride > 1) ? o->row_stride : 1;
     p.rows = rows;
@@ -393,7 +417,7 @@ int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nr
         if (!scene || !camera || !dev_out_rgb) throw std::invalid_argument("null argument");
         check_opts(opts);
         const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
-        RenderParams p = make_params(*camera, opts, rows);
+        RenderParams p = make_params(*camera, opts, rows, scene->flat);
         if (out_len < (size_t)rows * p.width * 3) throw std::invalid_argument("output buffer too small");
         const int dev = resolve_device(opts);
         DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
@@ -409,7 +433,7 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
         if (!scene || !camera || !out_rgb) throw std::invalid_argument("null argument");
         check_opts(opts);
         const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
-        RenderParams p = make_params(*camera, opts, rows);
+        RenderParams p = make_params(*camera, opts, rows, scene->flat);
         const size_t n = (size_t)rows * p.width * 3;
         if (out_len < n) throw std::invalid_argument("output buffer too small");
         if (n == 0) return NRT_OK;
@@ -516,7 +540,7 @@ int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, co
         if (!scene || !camera || !out || n < 5) throw std::invalid_argument("need scene, camera and out[5]");
         check_opts(opts);
         const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
-        RenderParams p = make_params(*camera, opts, rows);
+        RenderParams p = make_params(*camera, opts, rows, scene->flat);
         const size_t floats = (size_t)rows * p.width * 3;
         const int dev = resolve_device(opts);
         DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);

@@ -228,9 +228,10 @@ struct Philox {
     }
     // Render loop: one whole block per lane per iteration, counter
     // (pixel, sample, step): step 0 = camera ray, b + 1 = scatter at bounce b.
-    __device__ __forceinline__ uint4 block(uint32_t smp, uint32_t step) const {
+    __device__ __forceinline__ uint4 block(uint32_t smp, uint32_t step) const { return block_at(pix, smp, step); }
+    static __device__ __forceinline__ uint4 block_at(uint32_t pixel, uint32_t smp, uint32_t step) {
         uint32_t w[4];
-        philox4x32_10(pix, smp, step, 0u, 0u, 0u, w);
+        philox4x32_10(pixel, smp, step, 0u, 0u, 0u, w);
         return make_uint4(w[0], w[1], w[2], w[3]);
     }
 };
@@ -1189,26 +1190,56 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 }
 
 // ------------------------------------------------------------------ kernel
-// One thread per pixel.  Path regeneration: a lane starts its pixel's next
-// sample as soon as its current path terminates, so a wave no longer waits for
-// its longest path every sample; each lane still consumes its pixel's RNG
-// stream strictly in sample order and sums samples in order (camera.rs:325-331).
+// ChaCha8 (the reference's stream): one lane per pixel.  Path regeneration: a
+// lane starts its pixel's next sample as soon as its current path terminates,
+// so a wave no longer waits for its longest path every sample; each lane still
+// consumes its pixel's RNG stream strictly in sample order and sums samples in
+// order (camera.rs:325-331).
+//
+// Philox: a sample's random numbers depend only on (pixel, sample, bounce), so
+// a sample need not stay on one lane.  Waves are persistent: each takes groups of
+// p.wave_pixels consecutive pixels from a global queue and hands the group's
+// pixels x spp samples out from a wave-uniform counter; a lane whose path ends
+// claims the next unclaimed sample (ballot + mbcnt), so lanes stay busy until
+// the queue is empty instead of idling behind the lane with the longest run of
+// paths, and no wave idles while another still has pixels.  Sample radiance is
+// rounded to a 2^-k grid (p.acc_scale) and summed in f64 into per-pixel LDS
+// slots: sums of grid values below 2^53 are exact, hence independent of which
+// lane finished when, and frames are bitwise identical for every row partition,
+// group size and grid.
 //
 // PROF (diagnostic builds only, never timed): per-wave s_memtime stamps split
 // each loop iteration into camera-ray / trace / shading cycles, summed into
 // p.counters[0..3] = {iterations, camera, trace, shade} (+ [4] waves).
+//
 // Register budget: the f32 world-mode Philox kernel sits at the 80-VGPR edge of
 // 6 waves per SIMD; ask for 6 (the other variants keep the compiler's choice).
 template <typename R, class G, int MAXD>
 constexpr int min_waves_per_simd() { return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds) ? 6 : 1; }
-static_assert(BLOCK % 64 == 0, "stack / ring layouts assume whole waves");
+static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole waves");
+
+// Camera vector q of RenderParams: the f32 kernel takes the host-rounded copy
+// (kernel arguments stay in SGPRs), the f64 kernel the double.
+template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
+    if constexpr (sizeof(R) == 4) return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
+    else return ld3d<R>(d);
+}
+
+// Material of a hit, as the shading step needs it.
+template <typename R>
+struct MatV {
+    uint32_t kind = 0, tex = 0;
+    R param = R(0);
+    bool solid = false;  // f32 kernel: `color` is the (SolidColor) texture
+    V<R> color;
+};
 
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF = false>
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>()))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
-    // 6 Philox block, 7 scatter + accumulate
+    // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
     __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][8];
     if constexpr (PROF) {
         if (threadIdx.x < (BLOCK / 64) * 8) prof[threadIdx.x / 8][threadIdx.x % 8] = 0;
@@ -1219,70 +1250,330 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     auto leader = [&]() {  // first active lane of the wave
         return (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x;
     };
-    // dynamic LDS: [ChaCha8 ring][world-BVH stack][staged scene]
+    auto flush_prof = [&]() {
+        if constexpr (PROF) {
+            if (leader()) {
+                for (int c = 0; c < 8; ++c)
+                    if (c != 4) atomicAdd(&p.counters[c], prof[wave][c]);
+                atomicAdd(&p.counters[4], 1ull);
+            }
+        }
+    };
+    // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
+    const uint32_t acc_bytes = G::exact_stream ? 0u : (BLOCK / 64) * 2u * p.wave_pixels * (3u * (uint32_t)sizeof(double) + 4u);
     constexpr uint32_t stack_bytes = MAXD < 0 ? WBVH_STACK * BLOCK * sizeof(int32_t) : 0;
-    int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes) + threadIdx.x : nullptr;
+    int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
-    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + stack_bytes);
-
-    // Philox mode may split a pixel's samples over p.split adjacent lanes (sample s on
-    // lane s mod split, its own counter), summed at the end in a fixed shuffle tree.
-    const uint32_t split = G::exact_stream ? 1u : p.split;
-    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t i = p.pixel_begin + tid / split, sub = tid % split;
-    if (i >= p.pixel_end) return;
-    const uint32_t x = i % p.width;
-    const uint32_t row = i / p.width;
-    const uint32_t y = p.row_offset + row * p.row_stride;
-    const uint64_t n = (uint64_t)y * p.width + x;  // pixel index = RNG stream (camera.rs:320-323)
+    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
 
     G g;
-    g.init(n, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);
+    const V<R> top_left = cam3<R>(p, 0, p.top_left), du = cam3<R>(p, 1, p.pixel_delta_u);
+    const V<R> dv = cam3<R>(p, 2, p.pixel_delta_v), look_from = cam3<R>(p, 3, p.look_from);
+    const V<R> disk_u = cam3<R>(p, 4, p.defocus_disk_u), disk_v = cam3<R>(p, 5, p.defocus_disk_v);
+    const V<R> background = cam3<R>(p, 6, p.background);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform values live in SGPRs
 
-    auto cam = [&](int q, const double* d) {  // f32 kernel: host-rounded copies stay in SGPRs
-        if constexpr (sizeof(R) == 4) return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
-        else return ld3d<R>(d);
-    };
-    const V<R> top_left = cam(0, p.top_left), du = cam(1, p.pixel_delta_u), dv = cam(2, p.pixel_delta_v);
-    const V<R> look_from = cam(3, p.look_from), disk_u = cam(4, p.defocus_disk_u), disk_v = cam(5, p.defocus_disk_v);
-    const V<R> background = cam(6, p.background);
-
-    double ax = 0.0, ay = 0.0, az = 0.0;
-    uint32_t s = sub, b = 0, cur = 0;  // next sample of this lane, bounces of this path, current sample
+    uint32_t b = 0;  // bounces of this path
     bool bounced = false;
     Ray<R> ray;
     V<R> tp = mk(R(1), R(1), R(1));
-    // Philox mode: the block this lane consumes next (exactly one per path segment,
-    // computed by every shading lane at the same point: no divergent refills)
-    uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if constexpr (!G::exact_stream) w = g.block(sub, 0u);
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);  // Philox: this segment's block
 
-    // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
-    auto camera_ray = [&]() -> bool {
-        if (s >= p.spp) return false;
-        g.start_sample(s);
-        cur = s;
-        s += split;
-        R ox = R(0), oy = R(0);
-        if constexpr (G::exact_stream) {
+    auto albedo = [&](const MatV<R>& m, const Rec<R>& h) { return m.solid ? m.color : tex_color(sc, m.tex, h.u, h.v); };
+
+    auto material = [&](uint32_t mat) {  // the material table is LDS-resident: re-reading is cheap
+        MatV<R> m;
+        if constexpr (EXACT) {
+            const DMaterial dm = sc.materials[mat];
+            m.kind = dm.kind;
+            m.tex = dm.texture;
+            m.param = (R)dm.param;
+        } else {
+            const DMatFast dm = sc.mats_fast[mat];
+            m.kind = dm.kind;
+            m.tex = dm.texture;
+            m.param = dm.param;
+            m.solid = dm.solid != 0;
+            m.color = mk(dm.color[0], dm.color[1], dm.color[2]);
+        }
+        return m;
+    };
+
+    // The part of get_ray_color (camera.rs:269-300) before the scatter, after the
+    // closest-hit query of `ray` (`traced` false: the depth cap returned black, Q6):
+    // the hit record and material, and the radiance `contrib` added when the path
+    // ends here (background on a miss, emission on a light).  Returns true when the
+    // material scatters.  L = a0*(a1*(...*T)) is accumulated as a forward product tp.
+    auto surface = [&](bool traced, bool hit, const HitMin<R, MAXD>& hm, Rec<R>& h, MatV<R>& m,
+                       V<R>& contrib) -> bool {
+        contrib = mk(R(0), R(0), R(0));
+        if (!traced) return false;
+        if (!hit) {
+            contrib = tp * background;
+            return false;
+        }
+        h = make_record<R, MAXD, EXACT>(sc, ray, hm);
+        m = material(h.mat);
+        if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
+            const R k = bounced ? m.param : R(1.0);
+            contrib = tp * (k * albedo(m, h));
+            return false;
+        }
+        return true;
+    };
+
+    // Material::scatter (lambertian.rs:39-55, metal.rs:73-91, dielectric.rs:39-67)
+    // into the next `ray`; false when a metal absorbs the ray (emitted = 0).  The
+    // material is read again here rather than kept live across the RNG block.
+    auto scatter_ray = [&](const Rec<R>& h) -> bool {
+        const MatV<R> m = material(h.mat);
+        V<R> dir;
+        V<R> att = mk(R(1), R(1), R(1));
+        bool scattered = true;
+        if (m.kind == MAT_DIELECTRIC) {
+            const R ri = h.front ? R(1.0) / m.param : m.param;
+            const V<R> unit = normalize(ray.d);
+            const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
+            const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
+            bool refl = ri * sin_theta > R(1.0);
+            if (!refl) {
+                R r;
+                if constexpr (G::exact_stream) r = draw<R>(g, R(0.0), R(1.0));
+                else r = u01<R>(w.x);
+                refl = reflectance(cos_theta, ri) > r;
+            }
+            dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
+        } else {
+            V<R> rs;
+            if constexpr (G::exact_stream) rs = random_in_unit_sphere<R>(g);
+            else rs = unit_ball_inverse<R>(w.x, w.y, w.z);
+            if (m.kind == MAT_LAMBERTIAN) {
+                dir = h.n + rs;
+                if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
+            } else {  // metal: draws even when fuzz = 0 (Q5)
+                dir = normalize(reflect(ray.d, h.n)) + m.param * rs;
+                scattered = dot(dir, h.n) > R(0.0);
+            }
+            if (scattered) att = albedo(m, h);
+        }
+        if (!scattered) return false;
+        tp = tp * att;
+        ray.o = h.p;
+        ray.d = dir;
+        if constexpr (MAXD > 0) prep_ray<R, EXACT>(ray);  // world modes need no 1/d here
+        bounced = true;
+        ++b;
+        return true;
+    };
+
+    if constexpr (G::exact_stream) {
+        const uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
+        if (i >= p.pixel_end) return;
+        const uint32_t x = i % p.width;
+        const uint32_t y = p.row_offset + (i / p.width) * p.row_stride;
+        g.init((uint64_t)y * p.width + x, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);  // stream (camera.rs:320-323)
+        double ax = 0.0, ay = 0.0, az = 0.0;
+        uint32_t s = 0;  // next sample of the pixel
+
+        // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
+        auto camera_ray = [&]() -> bool {
+            if (s >= p.spp) return false;
+            g.start_sample(s);
+            ++s;
+            R ox = R(0), oy = R(0);
             if (p.spp > 1) {
                 ox = draw<R>(g, R(-0.5), R(0.5));
                 oy = draw<R>(g, R(-0.5), R(0.5));
             }
-        } else if (p.spp > 1) {
-            ox = u01<R>(w.x) - R(0.5);
-            oy = u01<R>(w.y) - R(0.5);
-        }
-        const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
-        if constexpr (G::exact_stream) {
+            const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
             const V<R> disk = random_in_unit_disk<R>(g);
             ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
+            prep_ray<R, EXACT>(ray);
+            tp = mk(R(1), R(1), R(1));
+            b = 0;
+            bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
+            return true;
+        };
+        // One shading step; true when the path continues with a new `ray`, otherwise
+        // the sample's radiance has been added to the pixel sum.
+        auto shade = [&](bool traced, bool hit, const HitMin<R, MAXD>& hm) -> bool {
+            const unsigned long long s0 = stamp();
+            Rec<R> h;
+            MatV<R> m;
+            V<R> contrib;
+            const bool scatter = surface(traced, hit, hm, h, m, contrib);
+            const unsigned long long s1 = stamp();
+            const bool cont = scatter && scatter_ray(h);
+            if (!cont) {  // metal absorption adds contrib = 0
+                ax += (double)contrib.x;
+                ay += (double)contrib.y;
+                az += (double)contrib.z;
+            }
+            if constexpr (PROF) {
+                const unsigned long long s2 = stamp();
+                if (leader()) {
+                    atomicAdd(&prof[wave][5], s1 - s0);
+                    atomicAdd(&prof[wave][7], s2 - s1);
+                }
+            }
+            return cont;
+        };
+
+        if constexpr (MAXD < 0) {
+            // World-BVH mode: traversal lengths differ widely between lanes, so each lane
+            // keeps its traversal state across rounds; the wave traverses until a ballot
+            // shows at least p.wave_wait lanes finished, then only those lanes shade and
+            // start their next segment (active-ray compaction within the wave).
+            static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
+            WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            bool active = camera_ray();
+            auto begin = [&]() {
+                // depth cap: no query, the lane waits to be shaded as black (Q6)
+                wbvh_begin(ts, b < p.max_bounces ? wbvh_root(gsc) : WBVH_DONE, ray);
+            };
+            if (active) begin();
+            const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
+            while (true) {
+                const unsigned long long t0 = stamp();
+                while (true) {
+                    const bool going = active && ts.busy();
+                    if (__ballot(going) == 0ull) break;
+                    if ((uint32_t)__popcll(__ballot(active && !ts.busy())) >= wait_min) break;
+                    if (going) wbvh_step(ts, gsc, ray, stack);
+                }
+                const unsigned long long t1 = stamp();
+                if (active && !ts.busy()) {
+                    HitMin<R, MAXD> hm;
+                    hm.t = ts.t_best;
+                    hm.prim = (uint32_t)ts.best;
+                    hm.depth = 0;
+                    if (!shade(b < p.max_bounces, ts.best >= 0, hm)) active = camera_ray();
+                    if (active) begin();
+                }
+                if constexpr (PROF) {
+                    const unsigned long long t2 = stamp();
+                    if (leader()) {
+                        atomicAdd(&prof[wave][0], 1ull);
+                        atomicAdd(&prof[wave][2], t1 - t0);
+                        atomicAdd(&prof[wave][3], t2 - t1);
+                    }
+                }
+                if (__ballot(active) == 0ull) break;
+            }
         } else {
+            bool fresh = true;
+            while (true) {
+                const unsigned long long t0 = stamp();
+                if (fresh) {
+                    if (!camera_ray()) break;
+                    fresh = false;
+                }
+                const unsigned long long t1 = stamp();
+                unsigned long long t2 = t1;
+                HitMin<R, MAXD> hm;
+                bool hit = false;
+                const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
+                if (traced) {
+                    // world list: the global tables through the scalar cache; records read LDS
+                    hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                    t2 = stamp();
+                }
+                fresh = !shade(traced, hit, hm);
+                if constexpr (PROF) {
+                    const unsigned long long t3 = stamp();
+                    if (leader()) {
+                        atomicAdd(&prof[wave][0], 1ull);
+                        atomicAdd(&prof[wave][1], t1 - t0);
+                        atomicAdd(&prof[wave][2], t2 - t1);
+                        atomicAdd(&prof[wave][3], t3 - t2);
+                    }
+                }
+            }
+        }
+        flush_prof();
+        const double spp = (double)p.spp;
+        float* o = p.out + 3ull * i;
+        o[0] = (float)(ax / spp);
+        o[1] = (float)(ay / spp);
+        o[2] = (float)(az / spp);
+    } else {
+        // ------------------------------------------------ Philox: per-wave sample pool
+        // Persistent waves.  A wave takes groups of P consecutive pixels from a global
+        // queue (one atomic per group) into a ring of two LDS slots and hands the
+        // P x spp samples of a group (index s * P + j; pixels past the end of the launch
+        // are padding samples that end at once) to whichever lane is free.  A group's
+        // pixel sums are written out when its last sample finishes.
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
+        const uint32_t GS = P * p.spp;  // samples per group (host: < 2^32)
+        // LDS per wave: 2 slots x P pixel sums (3 x f64) and 2 x P packed coordinates x | y << 16
+        double* acc = (double*)(lds + ring_bytes) + wv * 2u * P * 3u;
+        uint32_t* slot_xy = (uint32_t*)(lds + ring_bytes + (BLOCK / 64) * 2u * P * 3u * sizeof(double)) + wv * 2u * P;
+        constexpr uint32_t NO_GROUP = 0xFFFFFFFFu, PAD_XY = 0xFFFFFFFFu;
+        uint32_t gid0 = NO_GROUP, gid1 = NO_GROUP;  // group held by each slot (wave-uniform)
+        uint32_t done0 = 0, done1 = 0;              // finished samples per slot
+        uint32_t cs = 0, next = GS;                 // claiming from slot cs at index next
+        bool ready = false;                         // slot cs ^ 1 holds a group not yet claimed from
+        bool exhausted = false;                     // the queue is empty
+        auto fetch = [&]() {                        // uniform: take the next group into slot cs ^ 1
+            uint32_t gid = 0;
+            if (lane == 0) gid = atomicAdd(p.queue, 1u);
+            gid = __builtin_amdgcn_readlane(gid, 0);
+            exhausted = gid >= p.groups;  // (plain stores and selects: the flags stay in registers)
+            if (exhausted) return;
+            const uint32_t r = cs ^ 1u;
+            const uint32_t base = p.pixel_begin + gid * P;
+            double* a = acc + r * P * 3u;
+            uint32_t* xy = slot_xy + r * P;
+            for (uint32_t k = lane; k < P; k += 64u) {
+                a[3 * k] = a[3 * k + 1] = a[3 * k + 2] = 0.0;
+                const uint32_t il = base + k;
+                xy[k] = il >= p.pixel_end ? PAD_XY
+                                          : (il % p.width) | ((p.row_offset + (il / p.width) * p.row_stride) << 16);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            gid0 = r ? gid0 : gid;
+            gid1 = r ? gid : gid1;
+            done0 = r ? done0 : 0u;
+            done1 = r ? 0u : done1;
+            ready = true;
+        };
+        auto flush = [&](uint32_t gid, uint32_t r) {  // uniform: the group's last sample has finished
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const double* a = acc + r * P * 3u;
+            const double spp = (double)p.spp;
+            const uint32_t base = p.pixel_begin + gid * P;
+            for (uint32_t k = lane; k < P && base + k < p.pixel_end; k += 64u) {
+                float* o = p.out + 3ull * (base + k);
+                o[0] = (float)((a[3 * k] * p.acc_unscale) / spp);
+                o[1] = (float)((a[3 * k + 1] * p.acc_unscale) / spp);
+                o[2] = (float)((a[3 * k + 2] * p.acc_unscale) / spp);
+            }
+        };
+
+        uint32_t slot = 0, j = 0, cur = 0;  // ring slot, pixel in the group, sample index of this lane's path
+        uint32_t pxy = 0;                   // this path's pixel, x | y << 16
+        bool alive = false;                 // the lane holds a path
+        bool killed = false;                // absorbed by a metal (or padding): black, ends at the next shading step
+        auto pixel_index = [&]() { return (pxy >> 16) * p.width + (pxy & 0xFFFFu); };  // RNG stream (camera.rs:320-323)
+
+        // Camera::get_ray (camera.rs:244-267) for sample `cur` of pixel pxy; w holds its
+        // block (pixel, sample, 0).
+        auto camera = [&]() {
+            const uint32_t px = pxy & 0xFFFFu, py = pxy >> 16;
+            R ox = R(0), oy = R(0);
+            if (p.spp > 1) {
+                ox = u01<R>(w.x) - R(0.5);
+                oy = u01<R>(w.y) - R(0.5);
+            }
+            const V<R> point = (top_left + ((R)px + ox) * du) + ((R)py + oy) * dv;
             if (p.defocus) {
-                const uint4 wd = g.block(cur, PHILOX_STEP_DEFOCUS);
+                const uint4 wd = g.block_at(pixel_index(), cur, PHILOX_STEP_DEFOCUS);
                 const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
                 ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
             } else {
@@ -1290,208 +1581,130 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
             ray.d = point - ray.o;
             ray.time = u01<R>(w.z);
-        }
-        prep_ray<R, EXACT>(ray);
-        tp = mk(R(1), R(1), R(1));
-        b = 0;
-        bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
-        return true;
-    };
-
-    // One step of get_ray_color (camera.rs:269-300), L = a0*(a1*(...*T)), after the
-    // closest-hit query of `ray` (`traced` false: the depth cap returned black, Q6).
-    // Returns true when the path continues with a new `ray`; otherwise the sample's
-    // radiance has been added to the pixel sum.
-    auto shade = [&](bool traced, bool hit, const HitMin<R, MAXD>& hm) -> bool {
-        const unsigned long long s0 = stamp();
-        bool term = true, scatter = false;
-        V<R> contrib = mk(R(0), R(0), R(0));
-        Rec<R> h;
-        uint32_t mkind = 0, mtex = 0;
-        R mparam = R(0);
-        bool msolid = false;
-        V<R> mcolor = mk(R(0), R(0), R(0));
-        auto albedo = [&]() { return msolid ? mcolor : tex_color(sc, mtex, h.u, h.v); };
-        if (traced) {
-            if (!hit) {
-                contrib = tp * background;
-            } else {
-                h = make_record<R, MAXD, EXACT>(sc, ray, hm);
-                if constexpr (EXACT) {
-                    const DMaterial m = sc.materials[h.mat];
-                    mkind = m.kind;
-                    mtex = m.texture;
-                    mparam = (R)m.param;
-                } else {
-                    const DMatFast m = sc.mats_fast[h.mat];
-                    mkind = m.kind;
-                    mtex = m.texture;
-                    mparam = m.param;
-                    msolid = m.solid != 0;
-                    mcolor = mk(m.color[0], m.color[1], m.color[2]);
-                }
-                if (mkind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
-                    const R k = bounced ? mparam : R(1.0);
-                    contrib = tp * (k * albedo());
-                } else {
-                    scatter = true;
-                }
-            }
-        }
-        const unsigned long long s1 = stamp();
-        // Philox: this segment's block -- the scatter's (pixel, sample, bounce + 1), or, when
-        // the path ends here, the lane's next sample's camera block (pixel, sample + split, 0)
-        if constexpr (!G::exact_stream) w = g.block(scatter ? cur : cur + split, scatter ? b + 1 : 0u);
-        const unsigned long long s2 = stamp();
-        if (scatter) {
-            V<R> dir;
-            V<R> att = mk(R(1), R(1), R(1));
-            bool scattered = true;
-            if (mkind == MAT_DIELECTRIC) {  // dielectric.rs:39-67
-                const R ri = h.front ? R(1.0) / mparam : mparam;
-                const V<R> unit = normalize(ray.d);
-                const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
-                const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
-                bool refl = ri * sin_theta > R(1.0);
-                if (!refl) {
-                    R r;
-                    if constexpr (G::exact_stream) r = draw<R>(g, R(0.0), R(1.0));
-                    else r = u01<R>(w.x);
-                    refl = reflectance(cos_theta, ri) > r;
-                }
-                dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
-            } else {
-                V<R> rs;
-                if constexpr (G::exact_stream) rs = random_in_unit_sphere<R>(g);
-                else rs = unit_ball_inverse<R>(w.x, w.y, w.z);
-                if (mkind == MAT_LAMBERTIAN) {  // lambertian.rs:39-55
-                    dir = h.n + rs;
-                    if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
-                } else {  // metal.rs:73-91 (draws even when fuzz = 0, Q5)
-                    dir = normalize(reflect(ray.d, h.n)) + mparam * rs;
-                    scattered = dot(dir, h.n) > R(0.0);  // else absorbed: emitted = 0
-                }
-                if (scattered) att = albedo();
-            }
-            if (scattered) {
-                tp = tp * att;
-                ray.o = h.p;
-                ray.d = dir;
-                if constexpr (MAXD > 0) prep_ray<R, EXACT>(ray);  // world modes need no 1/d here
-                bounced = true;
-                ++b;
-                term = false;
-            } else if constexpr (!G::exact_stream) {
-                w = g.block(cur + split, 0u);  // absorbed by a metal: the next sample's camera block
-            }
-        }
-        if (term) {
-            ax += (double)contrib.x;
-            ay += (double)contrib.y;
-            az += (double)contrib.z;
-        }
-        if constexpr (PROF) {
-            const unsigned long long s3 = stamp();
-            if (leader()) {
-                atomicAdd(&prof[wave][5], s1 - s0);
-                atomicAdd(&prof[wave][6], s2 - s1);
-                atomicAdd(&prof[wave][7], s3 - s2);
-            }
-        }
-        return !term;
-    };
-
-    if constexpr (MAXD < 0) {
-        // World-BVH mode: traversal lengths differ widely between lanes, so each lane
-        // keeps its traversal state across rounds; the wave traverses until a ballot
-        // shows at least p.wave_wait lanes finished, then only those lanes shade and
-        // start their next segment (active-ray compaction within the wave).
-        static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
-        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        bool active = camera_ray();
-        auto begin = [&]() {
-            // depth cap: no query, the lane waits to be shaded as black (Q6)
-            wbvh_begin(ts, b < p.max_bounces ? wbvh_root(gsc) : WBVH_DONE, ray);
+            prep_ray<R, EXACT>(ray);
+            tp = mk(R(1), R(1), R(1));
+            b = 0;
+            bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
+            killed = false;
         };
-        if (active) begin();
+
+        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        auto begin = [&]() {  // world-BVH mode; depth cap / absorbed: no query (Q6)
+            if constexpr (MAXD < 0) wbvh_begin(ts, (!killed && b < p.max_bounces) ? wbvh_root(gsc) : WBVH_DONE, ray);
+        };
         const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
+
         while (true) {
-            const unsigned long long t0 = stamp();
-            while (true) {
-                const bool going = active && ts.busy();
-                if (__ballot(going) == 0ull) break;
-                if ((uint32_t)__popcll(__ballot(active && !ts.busy())) >= wait_min) break;
-                if (going) wbvh_step(ts, gsc, ray, stack);
+            // Group bookkeeping at the loop head, where little state is live: write out
+            // finished groups, and take the next group into the free slot as soon as
+            // fewer than a wave's worth of samples are left to claim.
+            if (gid0 != NO_GROUP && done0 == GS) {
+                flush(gid0, 0u);
+                gid0 = NO_GROUP;
             }
-            const unsigned long long t1 = stamp();
-            if (active && !ts.busy()) {
-                HitMin<R, MAXD> hm;
+            if (gid1 != NO_GROUP && done1 == GS) {
+                flush(gid1, 1u);
+                gid1 = NO_GROUP;
+            }
+            if (!exhausted && !ready && GS - next < 64u && (cs ? gid0 : gid1) == NO_GROUP) fetch();
+            if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
+            const unsigned long long t0 = stamp();
+            HitMin<R, MAXD> hm;
+            bool hit = false, sh, traced;
+            if constexpr (MAXD < 0) {
+                // World-BVH mode: lanes keep their traversal state across rounds; the wave
+                // traverses until a ballot shows >= p.wave_wait lanes finished, then only
+                // those lanes shade (active-ray compaction within the wave).
+                static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
+                while (true) {
+                    const bool going = alive && ts.busy();
+                    if (__ballot(going) == 0ull) break;
+                    if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
+                    if (going) wbvh_step(ts, gsc, ray, stack);
+                }
+                sh = alive && !ts.busy();
+                traced = sh && !killed && b < p.max_bounces;
                 hm.t = ts.t_best;
                 hm.prim = (uint32_t)ts.best;
                 hm.depth = 0;
-                if (!shade(b < p.max_bounces, ts.best >= 0, hm)) active = camera_ray();
-                if (active) begin();
-            }
-            if constexpr (PROF) {
-                const unsigned long long t2 = stamp();
-                if (leader()) {
-                    atomicAdd(&prof[wave][0], 1ull);
-                    atomicAdd(&prof[wave][2], t1 - t0);
-                    atomicAdd(&prof[wave][3], t2 - t1);
-                }
-            }
-            if (__ballot(active) == 0ull) break;
-        }
-    } else {
-        bool fresh = true;
-        while (true) {
-            const unsigned long long t0 = stamp();
-            if (fresh) {
-                if (!camera_ray()) break;
-                fresh = false;
+                hit = ts.best >= 0;
+            } else {
+                sh = alive;
+                traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
+                // world list: the global tables through the scalar cache; records read LDS
+                if (traced) hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
             }
             const unsigned long long t1 = stamp();
-            unsigned long long t2 = t1;
-            HitMin<R, MAXD> hm;
-            bool hit = false;
-            const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
-            if (traced) {
-                // world list: the global tables through the scalar cache; records read LDS
-                hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
-                t2 = stamp();
+            Rec<R> h;
+            MatV<R> m;
+            V<R> contrib = mk(R(0), R(0), R(0));
+            bool scatter = false;
+            if (sh) scatter = surface(traced, hit, hm, h, m, contrib);
+            const unsigned long long t2 = stamp();
+
+            // finished samples: radiance into the pixel's LDS sum, completion counts per slot
+            const bool ends = sh && !scatter;
+            if (ends && (contrib.x != R(0) || contrib.y != R(0) || contrib.z != R(0))) {
+                double* a = acc + (slot * P + j) * 3u;
+                atomicAdd(a, rint((double)contrib.x * p.acc_scale));
+                atomicAdd(a + 1, rint((double)contrib.y * p.acc_scale));
+                atomicAdd(a + 2, rint((double)contrib.z * p.acc_scale));
             }
-            fresh = !shade(traced, hit, hm);
+            done0 += (uint32_t)__popcll(__ballot(ends && slot == 0u));
+            done1 += (uint32_t)__popcll(__ballot(ends && slot == 1u));
+
+            // lanes without a path claim the next samples, in lane order: slot cs from
+            // `next`, then the group waiting in slot cs ^ 1
+            const bool want = ends || !alive;
+            const uint64_t em = __ballot(want);
+            const uint32_t nwant = (uint32_t)__popcll(em);
+            const uint32_t granted = min(nwant, (GS - next) + (ready ? GS : 0u));
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
+            const uint32_t claim = next + rank;
+            const uint32_t cs0 = cs;
+            next += granted;
+            if (next >= GS && ready) {
+                cs ^= 1u;
+                next -= GS;
+                ready = false;
+            }
+            if (want) {
+                alive = rank < granted;
+                if (alive) {
+                    const bool second = claim >= GS;
+                    slot = second ? cs0 ^ 1u : cs0;
+                    const uint32_t idx = second ? claim - GS : claim;
+                    j = idx & (P - 1u);
+                    cur = idx >> logP;
+                    pxy = slot_xy[slot * P + j];
+                }
+            }
+            // this segment's block: the scatter's (pixel, sample, bounce + 1) or the
+            // claimed sample's camera block (pixel', sample', 0)
+            w = g.block_at(pixel_index(), cur, scatter ? b + 1u : 0u);
+            const unsigned long long t3 = stamp();
+            if (scatter && !scatter_ray(h)) killed = true;
+            if (want && alive) {
+                camera();
+                killed = pxy == PAD_XY;  // padding sample: no pixel, ends at once
+            }
+            if ((sh || want) && alive) begin();
             if constexpr (PROF) {
-                const unsigned long long t3 = stamp();
+                const unsigned long long t4 = stamp();
+                const uint32_t busy = (uint32_t)__popcll(__ballot(sh));
                 if (leader()) {
                     atomicAdd(&prof[wave][0], 1ull);
-                    atomicAdd(&prof[wave][1], t1 - t0);
-                    atomicAdd(&prof[wave][2], t2 - t1);
-                    atomicAdd(&prof[wave][3], t3 - t2);
+                    atomicAdd(&prof[wave][1], (unsigned long long)busy);  // lane-iterations shading a path
+                    atomicAdd(&prof[wave][2], t1 - t0);
+                    atomicAdd(&prof[wave][3], t4 - t1);
+                    atomicAdd(&prof[wave][5], t2 - t1);
+                    atomicAdd(&prof[wave][6], t3 - t2);
+                    atomicAdd(&prof[wave][7], t4 - t3);
                 }
             }
         }
+        flush_prof();
     }
-    if constexpr (PROF) {
-        if (leader()) {
-            for (int c = 0; c < 8; ++c)
-                if (c != 4) atomicAdd(&p.counters[c], prof[wave][c]);
-            atomicAdd(&p.counters[4], 1ull);
-        }
-    }
-    if constexpr (!G::exact_stream) {
-        for (uint32_t m = 1; m < split; m <<= 1) {  // fixed order: every lane ends with the same sum
-            ax += __shfl_xor(ax, (int)m);
-            ay += __shfl_xor(ay, (int)m);
-            az += __shfl_xor(az, (int)m);
-        }
-        if (sub != 0) return;
-    }
-    const double spp = (double)p.spp;
-    float* o = p.out + 3ull * i;
-    o[0] = (float)(ax / spp);
-    o[1] = (float)(ay / spp);
-    o[2] = (float)(az / spp);
 }
 
 // First `count` next_u64 draws of a ChaCha8 / Philox stream (tests only).

@@ -1,6 +1,7 @@
 // Shared launch helper (included by each kernels_*.hip translation unit).
 #pragma once
 
+#include <algorithm>
 #include <stdexcept>
 
 #include "kernel.hpp"
@@ -10,29 +11,70 @@ namespace nrt {
 // Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
 constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 
+// Blocks the device keeps resident for one kernel variant.
+template <typename K>
+static uint64_t resident_blocks(K kernel, uint32_t lds_bytes) {
+    int per_cu = 0, dev_id = 0, cus = 0;
+    if (hipGetDevice(&dev_id) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, dev::BLOCK, lds_bytes) != hipSuccess ||
+        per_cu <= 0 || cus <= 0)
+        throw std::runtime_error("occupancy query failed for the render kernel");
+    return (uint64_t)per_cu * (uint64_t)cus;
+}
+
+// Philox: persistent waves (as many blocks as stay resident, capped by the group
+// count) over groups of P pixels.  Unless fixed (NRT_WAVE_PIXELS), P is the
+// smallest power of two with >= 1024 samples per group (a group must outlast the
+// longest path in flight for the ring of two to keep lanes busy; small groups keep
+// a wave's rays on few pixels), halved while the launch has fewer than two groups
+// per resident wave.  ChaCha8: one lane per pixel.
+template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF>
+static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint32_t lds_fixed, hipStream_t stream) {
+    auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, PROF>;
+    const uint32_t npix = p0.pixel_end - p0.pixel_begin;
+    if constexpr (G::exact_stream) {
+        hipLaunchKernelGGL(kernel, dim3((npix + dev::BLOCK - 1) / dev::BLOCK), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
+    } else {
+        RenderParams p = p0;
+        auto ring_bytes = [](uint32_t wp) { return (dev::BLOCK / 64) * 2u * wp * (3u * (uint32_t)sizeof(double) + 4u); };
+        uint32_t wp = p.wave_pixels;
+        if (!wp) {
+            wp = 1;
+            while (wp < 64 && (uint64_t)wp * p.spp < 1024) wp <<= 1;
+            const uint64_t w0 = resident_blocks(kernel, lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
+            while (wp > 1 && (npix + wp - 1) / wp < 2 * w0) wp >>= 1;
+        }
+        const uint64_t waves_res = resident_blocks(kernel, lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
+        p.wave_pixels = wp;
+        p.wave_pixels_log2 = 0;
+        while ((1u << p.wave_pixels_log2) < wp) ++p.wave_pixels_log2;
+        p.groups = (npix + wp - 1) / wp;
+        const uint64_t need = ((uint64_t)p.groups + dev::BLOCK / 64 - 1) / (dev::BLOCK / 64);
+        const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min(waves_res / (dev::BLOCK / 64), need));
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(dev::BLOCK), lds_fixed + ring_bytes(wp), stream, p, v);
+    }
+}
+
 template <typename R, class G, int MAXD, bool EXACT>
 static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_t stream) {
-    const uint32_t n = (p.pixel_end - p.pixel_begin) * (G::exact_stream ? 1u : p.split);  // lanes
-    const uint32_t blocks = (n + dev::BLOCK - 1) / dev::BLOCK;
+    // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
+    // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
-                          (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);  // + BVH stack
+                          (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v);
     if (p.counters) {  // diagnostic phase profile (nrt_debug_phase_profile)
         if constexpr (MAXD > 1) {
             throw std::runtime_error("phase profile: flat-instance scenes only");
         } else if (scene <= LDS_SCENE_LIMIT) {
-            hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true, true>), dim3(blocks), dim3(dev::BLOCK),
-                               ring + scene, stream, p, v);
+            launch_variant<R, G, MAXD, EXACT, true, true>(p, v, ring + scene, stream);
         } else {
-            hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, false, true>), dim3(blocks), dim3(dev::BLOCK),
-                               ring, stream, p, v);
+            launch_variant<R, G, MAXD, EXACT, false, true>(p, v, ring, stream);
         }
     } else if (scene <= LDS_SCENE_LIMIT) {
-        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, true>), dim3(blocks), dim3(dev::BLOCK), ring + scene,
-                           stream, p, v);
+        launch_variant<R, G, MAXD, EXACT, true, false>(p, v, ring + scene, stream);
     } else {
-        hipLaunchKernelGGL((dev::render_kernel<R, G, MAXD, EXACT, false>), dim3(blocks), dim3(dev::BLOCK), ring,
-                           stream, p, v);
+        launch_variant<R, G, MAXD, EXACT, false, false>(p, v, ring, stream);
     }
 }
 

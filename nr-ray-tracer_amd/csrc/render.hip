@@ -2,6 +2,8 @@
 // them and holds the host side (device buffers, launches).  No torch types.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "launch.hpp"
 
 #include <cstdlib>
@@ -47,7 +49,12 @@ struct DeviceScene {
     bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
+    // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS counters and
+    // zeroes it on its own stream (up to QUEUE_SLOTS launches may be in flight at once).
+    unsigned int* queues = nullptr;
+    mutable std::atomic<uint32_t> queue_next{0};
 };
+constexpr uint32_t QUEUE_SLOTS = 256;
 
 int gpu_device_count() {
     int n = 0;
@@ -108,6 +115,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.wbvh.nodes.size()};
         ds->wbvh_ok = fs.wbvh_ok;
         ds->wbvh_prims = wbp;
+        check(hipMalloc((void**)&ds->queues, QUEUE_SLOTS * sizeof(unsigned int)), "hipMalloc(queues)");
+        track(ds->queues, QUEUE_SLOTS * sizeof(unsigned int));
+        check(hipMemset(ds->queues, 0, QUEUE_SLOTS * sizeof(unsigned int)), "hipMemset(queues)");
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();
         ds->world_ok = fs.world_ok;
         ds->world_units = fs.world_units;
@@ -156,7 +166,12 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     if (p.pixel_end <= p.pixel_begin) return;
     if (p.width == 0) throw std::runtime_error("width must be > 0");
     hipStream_t stream = (hipStream_t)stream_ptr;
-    if (precision == 0) launch_exact(p, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, stream);
+    RenderParams q = p;
+    if (rng == RNG_PHILOX) {  // group size and count: launch_variant (launch_impl.hpp)
+        q.queue = ds->queues + ds->queue_next.fetch_add(1) % QUEUE_SLOTS;
+        check(hipMemsetAsync(q.queue, 0, sizeof(unsigned int), stream), "hipMemsetAsync(queue)");
+    }
+    if (precision == 0) launch_exact(q, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, stream);
     else {
         const int maxd = gpu_fast_maxd(ds, trace);
         DSceneView<float> v = ds->v32;  // stage (LDS) only the tables this mode reads
@@ -171,7 +186,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         } else {
             v.n_wprims = 0;
         }
-        launch_fast(p, v, rng, maxd, stream);
+        launch_fast(q, v, rng, maxd, stream);
     }
     check(hipGetLastError(), "render kernel launch");
 }

@@ -22,7 +22,12 @@ struct RenderParams {
     float camf[7][3];
     uint32_t defocus;  // 0: defocus disk is zero (defocus_angle <= 0), disk draws only feed the origin
     uint32_t wave_wait;  // world-BVH mode: lanes that must finish traversal before a shading round
-    uint32_t split;      // Philox mode: lanes per pixel (power of two <= 64); 1 for ChaCha8
+    // Philox mode: pixels per wave (power of two <= 64, wave_pixels * spp < 2^32) and
+    // the 2^k grid each sample's radiance is rounded to before the exact f64 sum.
+    uint32_t wave_pixels, wave_pixels_log2;
+    double acc_scale, acc_unscale;  // 2^k, 2^-k
+    uint32_t groups;                // Philox: pixel groups (of wave_pixels) in this launch
+    unsigned int* queue;            // Philox: group queue head (device, zeroed before the launch)
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;

@@ -364,12 +364,20 @@ class Scene:
         out = (C.c_uint64 * 8)()
         _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 8))
         iters, cam_c, trace_c, shade_c, waves, rec_c, rng_c, scat_c = list(out)
-        tot = max(cam_c + trace_c + shade_c, 1)
-        return {"iterations_per_wave": iters / max(waves, 1), "camera_share": cam_c / tot,
-                "trace_share": trace_c / tot, "shade_share": shade_c / tot,
-                "shade_record_share": rec_c / tot, "shade_rng_share": rng_c / tot,
-                "shade_scatter_share": scat_c / tot,
-                "cycles_per_iteration": tot / max(iters, 1), "waves": waves}
+        res = {"iterations_per_wave": iters / max(waves, 1), "waves": waves}
+        if rng == "philox":
+            # sample-pool loop: camera rays are part of the shading step; slot 1 counts
+            # lane-iterations that shaded a path (lane occupancy of the loop)
+            tot = max(trace_c + shade_c, 1)
+            res["lane_occupancy"] = cam_c / max(64 * iters, 1)
+            res["camera_share"] = 0.0
+        else:
+            tot = max(cam_c + trace_c + shade_c, 1)
+            res["camera_share"] = cam_c / tot
+        res.update({"trace_share": trace_c / tot, "shade_share": shade_c / tot,
+                    "shade_record_share": rec_c / tot, "shade_rng_share": rng_c / tot,
+                    "shade_scatter_share": scat_c / tot, "cycles_per_iteration": tot / max(iters, 1)})
+        return res
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",
                       rng: str = "philox", device: int = -1, row_offset: int = 0, row_stride: int = 1,

@@ -80,14 +80,31 @@ def test_f64_chacha8_matches_oracle(scene, w, h, spp, bounces):
 
 
 def test_philox_row_interleave_is_bitwise_identical():
-    # split lanes per pixel are fixed per frame: any row partition sums samples in the same order
+    # Philox samples are claimed from a per-wave pool by whichever lane is free and summed
+    # exactly (radiance on a 2^-k grid): any row partition gives the same bits
     scene, w, h, spp = "scenes/cornell-box-scene.json", 32, 21, 16
     s = load(scene, w, h, spp)
     full = s.render(precision="f32", rng="philox")
-    for stride in (2, 8):
+    for stride in (2, 3, 8):
         for off in range(stride):
             part = s.render(precision="f32", rng="philox", row_offset=off, row_stride=stride)
             np.testing.assert_array_equal(part, full[off::stride])
+
+
+@pytest.mark.parametrize("scene,precision,trace", [
+    ("scenes/cornell-box-scene.json", "f32", "auto"),
+    ("scenes/cornell-box-scene.json", "f32", "bvh"),
+    ("scenes/cornell-box-scene.json", "f64", "auto"),
+    ("scenes/spheres.toml", "f32", "world-bvh"),
+])
+def test_philox_wave_size_is_bitwise_identical(monkeypatch, scene, precision, trace):
+    # pixels per wave (pool size, lane <-> sample assignment, claim order) leave every bit unchanged
+    s = load(scene, 40, 23, 24, 12)
+    full = s.render(precision=precision, rng="philox", trace=trace)
+    assert np.all(np.isfinite(full)) and full.max() > 0
+    for wp in ("1", "4", "64"):
+        monkeypatch.setenv("NRT_WAVE_PIXELS", wp)
+        np.testing.assert_array_equal(s.render(precision=precision, rng="philox", trace=trace), full)
 
 
 def test_row_interleave_is_bitwise_identical():
