@@ -206,6 +206,10 @@ int nrt_image_to_rgb8(const float* rgb, size_t n_floats, float gamma, uint8_t* o
  * (ChaCha8: stream = pixel index; Philox: counter (pixel, sample, pair)). */
 int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out);
 
+/* Tests: the 256-entry permutation table of the Perlin source for `seed` (noise 0.9.0
+ * PermutationTable::new, used by the Noise / Marble textures, lib/textures/noise.rs:85-92). */
+int nrt_debug_perlin_permutation(uint32_t seed, uint8_t* out);
+
 /* Diagnostics: one render with per-wave s_memtime stamps; out[0..4] = {loop
  * iterations, camera-ray cycles, trace cycles, shading cycles, waves} summed over
  * waves, and with n >= 8 out[5..7] = the shading cycles split into {hit record +

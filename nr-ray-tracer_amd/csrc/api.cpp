@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "flatten.hpp"
+#include "noise.hpp"
 #include "gpu.hpp"
 #include "scene.hpp"
 #include "scene_config.hpp"
@@ -206,10 +207,16 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     {
         double emit = 0.0, alb = 1.0;
         for (int k = 0; k < 3; ++k) emit = std::fmax(emit, std::fabs(c.background_color[k]));
-        double texmax = 1.0;  // image texels are <= 1
-        for (const DTexture& t : f.textures)
+        double texmax = 1.0;  // image texels and marble are <= 1
+        for (const DTexture& t : f.textures) {
             if (t.kind == TEX_SOLID)
                 for (int k = 0; k < 3; ++k) texmax = std::fmax(texmax, std::fabs(t.color[k]));
+            if (t.kind == TEX_NOISE) {  // |Fbm| <= scale x sum_k |persistence|^k (|perlin| <= 1)
+                double amp = 0.0, pk = 1.0;
+                for (uint32_t k = 0; k < t.a; ++k, pk *= std::fabs(t.color[2])) amp += pk;
+                texmax = std::fmax(texmax, std::fabs(t.scale) * amp);
+            }
+        }
         for (const DMaterial& m : f.materials) {
             if (m.kind == MAT_DIFFUSE_LIGHT) emit = std::fmax(emit, std::fmax(1.0, std::fabs(m.param)) * texmax);
         }
@@ -562,6 +569,14 @@ int nrt_debug_phase_profile(const nrt_scene* scene, const nrt_camera* camera, co
         }
         device_free(img, dev);
         device_free(ctr, dev);
+        return NRT_OK;
+    });
+}
+
+int nrt_debug_perlin_permutation(uint32_t seed, uint8_t* out) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!out) throw std::invalid_argument("null output");
+        perlin_permutation(seed, out);
         return NRT_OK;
     });
 }

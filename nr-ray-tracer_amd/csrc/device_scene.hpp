@@ -37,7 +37,7 @@ constexpr uint32_t WKIND_BITS = 3, WKIND_MASK = 7;
 enum : uint32_t { PRIM_QUAD_X = 4, PRIM_QUAD_Y = 5, PRIM_QUAD_Z = 6, PRIM_ABOX = 7 };
 enum : uint32_t { XF_TRANSLATE = 0, XF_ROTATE = 1, XF_SCALE = 2 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
-enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2 };
+enum : uint32_t { TEX_SOLID = 0, TEX_IMAGE = 1, TEX_CHECKER = 2, TEX_NOISE = 3, TEX_MARBLE = 4 };
 
 constexpr int32_t NODE_END = -1;
 constexpr int MAX_INSTANCE_DEPTH = 4;
@@ -200,11 +200,12 @@ struct alignas(16) DMatFast {
 
 struct alignas(16) DTexture {
     uint32_t kind;
-    uint32_t a, b;     // image: width, height; checker: even, odd texture ids
+    uint32_t a, b;     // image: width, height; checker: even, odd texture ids; noise/marble: octaves, seed
     uint32_t pad;
-    uint64_t offset;   // image: first texel (float index / 3) in the texel array
-    double color[3];   // solid colour
-    double scale;      // checker scale
+    uint64_t offset;   // image: first texel (float index / 3) in the texel array; noise/marble: first
+                       // permutation table (octaves x 256 floats 0..255) likewise
+    double color[3];   // solid colour; noise/marble: frequency, lacunarity, persistence
+    double scale;      // checker scale; noise/marble: Fbm scale factor
 };
 
 // What the kernel gets: device pointers + sizes (per precision).

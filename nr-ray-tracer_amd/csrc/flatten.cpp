@@ -58,9 +58,28 @@ struct Flattener {
                 d.b = o;
                 break;
             }
-            case Texture::Unsupported:
-                throw std::runtime_error("texture kind '" + t->note +
-                                         "' (Perlin noise) is outside the accelerated path (SURVEY.md §8f rank 4)");
+            case Texture::Noise:
+            case Texture::Marble: {
+                // Abs<Fbm<Perlin>>: one permutation table per octave (seed + k), stored
+                // in the texel array as floats 0..255 (exact), starting on a triplet
+                d.kind = t->kind == Texture::Noise ? TEX_NOISE : TEX_MARBLE;
+                const FbmParams& f = t->fbm;
+                d.a = f.octaves;
+                d.b = f.seed;
+                d.color[0] = f.frequency;
+                d.color[1] = f.lacunarity;
+                d.color[2] = f.persistence;
+                d.scale = fbm_scale_factor(f.persistence, f.octaves);
+                while (out.texels.size() % 3) out.texels.push_back(0.f);
+                d.offset = out.texels.size() / 3;
+                uint8_t perm[256];
+                for (uint32_t k = 0; k < f.octaves; ++k) {
+                    perlin_permutation(f.seed + k, perm);  // Fbm build_sources: seed + k (u32 wrap)
+                    for (int i = 0; i < 256; ++i) out.texels.push_back((float)perm[i]);
+                }
+                while (out.texels.size() % 3) out.texels.push_back(0.f);
+                break;
+            }
         }
         const uint32_t id = (uint32_t)out.textures.size();
         out.textures.push_back(d);
@@ -931,7 +950,17 @@ void dump_tex(std::string& s, const Texture* t) {
             dump_tex(s, t->odd.get());
             s += " )";
             break;
-        case Texture::Unsupported: s += " UNSUPPORTED " + t->note; break;
+        case Texture::Noise:
+        case Texture::Marble: {
+            char buf[64];
+            const FbmParams& f = t->fbm;
+            snprintf(buf, sizeof buf, t->kind == Texture::Noise ? " NOISE %u %u" : " MARBLE %u %u", f.seed, f.octaves);
+            s += buf;
+            hex(s, f.frequency);
+            hex(s, f.lacunarity);
+            hex(s, f.persistence);
+            break;
+        }
     }
 }
 

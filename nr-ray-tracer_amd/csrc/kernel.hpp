@@ -1117,12 +1117,89 @@ __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray
 }
 
 // ----------------------------------------------------------------- shading
-// Texture::get_color (solid_color.rs:45-53, image.rs:83-94, checker.rs:170-184)
-template <typename R>
-__device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v) {
+// Perlin textures in f64 (noise 0.9.0 as restated in noise.hpp).  `perm` is the
+// octave's permutation table (256 floats 0..255 in the texel array).
+__device__ __forceinline__ double perlin_grad(uint32_t h, double x, double y, double z) {
+    // noise 0.9 perlin_3d gradient_dot_v: every case is (±a) + (±b) with a in {x, y}, b in
+    // {y, z}; the 16 cases as bit masks over h & 15
+    const uint32_t bit = 1u << (h & 15u);
+    const double a = (0xCF00u & bit) ? y : x, b = (0x300Fu & bit) ? y : z;
+    return ((0xEAAAu & bit) ? -a : a) + ((0x8CCCu & bit) ? -b : b);
+}
+__device__ __forceinline__ double perlin3(const float* perm, double x, double y, double z) {
+    auto P = [&](uint32_t i) { return (uint32_t)perm[i]; };
+    const double fx = floor(x), fy = floor(y), fz = floor(z);
+    const uint32_t ix = (uint32_t)(long long)fx & 255u, iy = (uint32_t)(long long)fy & 255u,
+                   iz = (uint32_t)(long long)fz & 255u;
+    const double dx = x - fx, dy = y - fy, dz = z - fz;
+    const uint32_t ix1 = (ix + 1u) & 255u, iy1 = (iy + 1u) & 255u, iz1 = (iz + 1u) & 255u;
+    const uint32_t a0 = P(ix), a1 = P(ix1);
+    const uint32_t b00 = P(a0 ^ iy), b10 = P(a1 ^ iy), b01 = P(a0 ^ iy1), b11 = P(a1 ^ iy1);
+    const double g000 = perlin_grad(P(b00 ^ iz), dx, dy, dz);
+    const double g100 = perlin_grad(P(b10 ^ iz), dx - 1.0, dy, dz);
+    const double g010 = perlin_grad(P(b01 ^ iz), dx, dy - 1.0, dz);
+    const double g110 = perlin_grad(P(b11 ^ iz), dx - 1.0, dy - 1.0, dz);
+    const double g001 = perlin_grad(P(b00 ^ iz1), dx, dy, dz - 1.0);
+    const double g101 = perlin_grad(P(b10 ^ iz1), dx - 1.0, dy, dz - 1.0);
+    const double g011 = perlin_grad(P(b01 ^ iz1), dx, dy - 1.0, dz - 1.0);
+    const double g111 = perlin_grad(P(b11 ^ iz1), dx - 1.0, dy - 1.0, dz - 1.0);
+    auto quintic = [](double t) { return t * t * t * (t * (t * 6.0 - 15.0) + 10.0); };
+    const double a = quintic(dx), b = quintic(dy), c = quintic(dz);
+    const double k0 = g000, k1 = g100 - g000, k2 = g010 - g000, k3 = g001 - g000;
+    const double k4 = g000 + g110 - g100 - g010, k5 = g000 + g101 - g100 - g001;
+    const double k6 = g000 + g011 - g010 - g001;
+    const double k7 = g100 + g010 + g001 + g111 - g000 - g110 - g101 - g011;
+    const double r = k0 + k1 * a + k2 * b + k3 * c + k4 * a * b + k5 * a * c + k6 * b * c + k7 * a * b * c;
+    const double s = r * 1.1547005383792515;  // 1 / (sqrt(3) / 2)
+    return s < -1.0 ? -1.0 : (s > 1.0 ? 1.0 : s);
+}
+__device__ __forceinline__ double powi_rt(double a, uint32_t b) {  // f64::powi, b >= 0 (__powidf2)
+    double r = 1.0;
+    while (true) {
+        if (b & 1u) r *= a;
+        b /= 2u;
+        if (b == 0u) break;
+        a *= a;
+    }
+    return r;
+}
+// Abs<Fbm<Perlin>>::get (noise.rs:136-144, marble.rs:87-96), then the Noise / Marble
+// colour (compiled into the KF_PERLIN kernel variants only).
+__device__ __forceinline__ double perlin_texture(const float* texels, const DTexture& t, double x, double y, double z) {
+    const float* perm = texels + 3ull * t.offset;
+    const double pz = z;
+    x = x * t.color[0];
+    y = y * t.color[0];
+    z = z * t.color[0];
+    double result = 0.0;
+    for (uint32_t k = 0; k < t.a; ++k) {
+        double signal = perlin3(perm + 256u * k, x, y, z);
+        signal = signal * powi_rt(t.color[2], k);
+        result = result + signal;
+        x = x * t.color[1];
+        y = y * t.color[1];
+        z = z * t.color[1];
+    }
+    const double n = fabs(result * t.scale);
+    return t.kind == TEX_NOISE ? n : (1.0 + sin(t.color[0] * pz + 10.0 * n)) / 2.0;
+}
+
+// Texture::get_color (solid_color.rs:45-53, image.rs:83-94, checker.rs:170-184,
+// noise.rs:136-144, marble.rs:87-96); `p` = the world-space hit point
+template <typename R, bool PERLIN>
+__device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> p) {
     for (int guard = 0; guard < 64; ++guard) {
         const DTexture& t = sc.textures[tid];
         if (t.kind == TEX_SOLID) return ld3d<R>(t.color);
+        if (t.kind == TEX_NOISE || t.kind == TEX_MARBLE) {
+            // (the host launches a PERLIN variant whenever the scene holds one of these)
+            if constexpr (PERLIN) {
+                const double c = perlin_texture(sc.texels, t, (double)p.x, (double)p.y, (double)p.z);
+                return mk((R)c, (R)c, (R)c);
+            } else {
+                return mk(R(0), R(0), R(0));
+            }
+        }
         if (t.kind == TEX_IMAGE) {
             const R cu = u < R(0) ? R(0) : (u > R(1) ? R(1) : u);  // f64::clamp keeps NaN
             const R cv = v < R(0) ? R(0) : (v > R(1) ? R(1) : v);
@@ -1214,8 +1291,19 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 //
 // Register budget: the f32 world-mode Philox kernel sits at the 80-VGPR edge of
 // 6 waves per SIMD; ask for 6 (the other variants keep the compiler's choice).
+//
+// Kernel variant flags: KF_PROF = phase-profile stamps (diagnostics), KF_PERLIN = the
+// scene has Noise / Marble textures (their f64 Fbm code is only compiled into the
+// variants that need it: it would raise the register budget of every other scene).
+constexpr int KF_PROF = 1, KF_PERLIN = 2;
+
 template <typename R, class G, int MAXD>
-constexpr int min_waves_per_simd() { return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds) ? 6 : 1; }
+constexpr int min_waves_per_simd(bool perlin = false) {
+#ifndef NRT_WORLD_LIST_WAVES
+#define NRT_WORLD_LIST_WAVES 6
+#endif
+    return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !perlin) ? NRT_WORLD_LIST_WAVES : 1;
+}
 static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole waves");
 
 // Camera vector q of RenderParams: the f32 kernel takes the host-rounded copy
@@ -1234,9 +1322,11 @@ struct MatV {
     V<R> color;
 };
 
-template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF = false>
-__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>()))
+template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0>
+__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>((KFLAGS & KF_PERLIN) != 0)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
+    constexpr bool PROF = (KFLAGS & KF_PROF) != 0;
+    constexpr bool PERLIN = (KFLAGS & KF_PERLIN) != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
     // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
@@ -1280,7 +1370,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     V<R> tp = mk(R(1), R(1), R(1));
     uint4 w = make_uint4(0u, 0u, 0u, 0u);  // Philox: this segment's block
 
-    auto albedo = [&](const MatV<R>& m, const Rec<R>& h) { return m.solid ? m.color : tex_color(sc, m.tex, h.u, h.v); };
+    auto albedo = [&](const MatV<R>& m, const Rec<R>& h) { return m.solid ? m.color : tex_color<R, PERLIN>(sc, m.tex, h.u, h.v, h.p); };
 
     auto material = [&](uint32_t mat) {  // the material table is LDS-resident: re-reading is cheap
         MatV<R> m;
@@ -1518,11 +1608,33 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t cs = 0, next = GS;                 // claiming from slot cs at index next
         bool ready = false;                         // slot cs ^ 1 holds a group not yet claimed from
         bool exhausted = false;                     // the queue is empty
+        // Per-XCD queue heads: head x hands out the x-th contiguous eighth of the groups,
+        // and a wave pulls from its own XCD's head first (then the next heads in turn), so
+        // neighbouring groups, whose 12-B pixels share cache lines, are written out by one
+        // XCD's L2 and no head is contended by more than one XCD's waves until the tail.
+        // The XCD id only places work (any wave may pull from any head): never correctness.
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        uint32_t qk = 0;  // heads found empty so far (wave-uniform)
         auto fetch = [&]() {                        // uniform: take the next group into slot cs ^ 1
-            uint32_t gid = 0;
-            if (lane == 0) gid = atomicAdd(p.queue, 1u);
+            uint32_t gid = 0xFFFFFFFFu;
+            if (lane == 0) {
+                for (; qk < QUEUE_HEADS; ++qk) {
+                    const uint32_t x = (xcc + qk) & (QUEUE_HEADS - 1u);
+                    const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
+                    const uint32_t hi = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS);
+                    if (hi > lo) {
+                        const uint32_t t = atomicAdd(p.queue + x * QUEUE_STRIDE, 1u);
+                        if (t < hi - lo) {
+                            gid = lo + t;
+                            break;
+                        }
+                    }
+                }
+            }
             gid = __builtin_amdgcn_readlane(gid, 0);
-            exhausted = gid >= p.groups;  // (plain stores and selects: the flags stay in registers)
+            qk = __builtin_amdgcn_readlane(qk, 0);
+            exhausted = gid == 0xFFFFFFFFu;  // (plain stores and selects: the flags stay in registers)
             if (exhausted) return;
             const uint32_t r = cs ^ 1u;
             const uint32_t base = p.pixel_begin + gid * P;
@@ -1548,12 +1660,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const double* a = acc + r * P * 3u;
             const double spp = (double)p.spp;
             const uint32_t base = p.pixel_begin + gid * P;
-            for (uint32_t k = lane; k < P && base + k < p.pixel_end; k += 64u) {
-                float* o = p.out + 3ull * (base + k);
-                o[0] = (float)((a[3 * k] * p.acc_unscale) / spp);
-                o[1] = (float)((a[3 * k + 1] * p.acc_unscale) / spp);
-                o[2] = (float)((a[3 * k + 2] * p.acc_unscale) / spp);
-            }
+            // the group's pixels are 3 x P contiguous floats in LDS and in the framebuffer:
+            // one coalesced dword per lane (16-B stores cost the shading loop a spill)
+            const uint32_t nf = 3u * min(P, p.pixel_end - base);
+            float* o = p.out + 3ull * base;
+            for (uint32_t l = lane; l < nf; l += 64u) o[l] = (float)((a[l] * p.acc_unscale) / spp);
         };
 
         uint32_t slot = 0, j = 0, cur = 0;  // ring slot, pixel in the group, sample index of this lane's path

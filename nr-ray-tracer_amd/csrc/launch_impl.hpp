@@ -29,9 +29,9 @@ static uint64_t resident_blocks(K kernel, uint32_t lds_bytes) {
 // longest path in flight for the ring of two to keep lanes busy; small groups keep
 // a wave's rays on few pixels), halved while the launch has fewer than two groups
 // per resident wave.  ChaCha8: one lane per pixel.
-template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, bool PROF>
+template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS>
 static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint32_t lds_fixed, hipStream_t stream) {
-    auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, PROF>;
+    auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, KFLAGS>;
     const uint32_t npix = p0.pixel_end - p0.pixel_begin;
     if constexpr (G::exact_stream) {
         hipLaunchKernelGGL(kernel, dim3((npix + dev::BLOCK - 1) / dev::BLOCK), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
@@ -57,24 +57,31 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
 }
 
 template <typename R, class G, int MAXD, bool EXACT>
-static void launch_one(const RenderParams& p, const DSceneView<R>& v, hipStream_t stream) {
+static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perlin, hipStream_t stream) {
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
                           (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v);
+    using dev::KF_PERLIN;
+    using dev::KF_PROF;
     if (p.counters) {  // diagnostic phase profile (nrt_debug_phase_profile)
         if constexpr (MAXD > 1) {
             throw std::runtime_error("phase profile: flat-instance scenes only");
+        } else if (perlin) {
+            throw std::runtime_error("phase profile: scenes without Perlin textures only");
         } else if (scene <= LDS_SCENE_LIMIT) {
-            launch_variant<R, G, MAXD, EXACT, true, true>(p, v, ring + scene, stream);
+            launch_variant<R, G, MAXD, EXACT, true, KF_PROF>(p, v, ring + scene, stream);
         } else {
-            launch_variant<R, G, MAXD, EXACT, false, true>(p, v, ring, stream);
+            launch_variant<R, G, MAXD, EXACT, false, KF_PROF>(p, v, ring, stream);
         }
+    } else if (perlin) {
+        if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, KF_PERLIN>(p, v, ring + scene, stream);
+        else launch_variant<R, G, MAXD, EXACT, false, KF_PERLIN>(p, v, ring, stream);
     } else if (scene <= LDS_SCENE_LIMIT) {
-        launch_variant<R, G, MAXD, EXACT, true, false>(p, v, ring + scene, stream);
+        launch_variant<R, G, MAXD, EXACT, true, 0>(p, v, ring + scene, stream);
     } else {
-        launch_variant<R, G, MAXD, EXACT, false, false>(p, v, ring, stream);
+        launch_variant<R, G, MAXD, EXACT, false, 0>(p, v, ring, stream);
     }
 }
 

@@ -47,10 +47,12 @@ struct DeviceScene {
     bool world_ok = false;  // fast kernel may run in world-space mode (v32.wprims)
     uint64_t world_units = 0;
     bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
+    bool perlin = false;    // Noise / Marble textures present (KF_PERLIN kernel variants)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
-    // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS counters and
-    // zeroes it on its own stream (up to QUEUE_SLOTS launches may be in flight at once).
+    // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS sets of
+    // QUEUE_HEADS per-XCD heads and zeroes it on its own stream (up to QUEUE_SLOTS
+    // launches may be in flight at once).
     unsigned int* queues = nullptr;
     mutable std::atomic<uint32_t> queue_next{0};
 };
@@ -114,10 +116,12 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     fs.wbvh.root4, fs.wbvh.root,
                                     (uint32_t)fs.wbvh.nodes.size()};
         ds->wbvh_ok = fs.wbvh_ok;
+        for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->wbvh_prims = wbp;
-        check(hipMalloc((void**)&ds->queues, QUEUE_SLOTS * sizeof(unsigned int)), "hipMalloc(queues)");
-        track(ds->queues, QUEUE_SLOTS * sizeof(unsigned int));
-        check(hipMemset(ds->queues, 0, QUEUE_SLOTS * sizeof(unsigned int)), "hipMemset(queues)");
+        const size_t qbytes = (size_t)QUEUE_SLOTS * QUEUE_HEADS * QUEUE_STRIDE * sizeof(unsigned int);
+        check(hipMalloc((void**)&ds->queues, qbytes), "hipMalloc(queues)");
+        track(ds->queues, qbytes);
+        check(hipMemset(ds->queues, 0, qbytes), "hipMemset(queues)");
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();
         ds->world_ok = fs.world_ok;
         ds->world_units = fs.world_units;
@@ -168,10 +172,11 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     hipStream_t stream = (hipStream_t)stream_ptr;
     RenderParams q = p;
     if (rng == RNG_PHILOX) {  // group size and count: launch_variant (launch_impl.hpp)
-        q.queue = ds->queues + ds->queue_next.fetch_add(1) % QUEUE_SLOTS;
-        check(hipMemsetAsync(q.queue, 0, sizeof(unsigned int), stream), "hipMemsetAsync(queue)");
+        const size_t qwords = (size_t)QUEUE_HEADS * QUEUE_STRIDE;
+        q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;
+        check(hipMemsetAsync(q.queue, 0, qwords * sizeof(unsigned int), stream), "hipMemsetAsync(queue)");
     }
-    if (precision == 0) launch_exact(q, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, stream);
+    if (precision == 0) launch_exact(q, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, ds->perlin, stream);
     else {
         const int maxd = gpu_fast_maxd(ds, trace);
         DSceneView<float> v = ds->v32;  // stage (LDS) only the tables this mode reads
@@ -186,7 +191,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         } else {
             v.n_wprims = 0;
         }
-        launch_fast(q, v, rng, maxd, stream);
+        launch_fast(q, v, rng, maxd, ds->perlin, stream);
     }
     check(hipGetLastError(), "render kernel launch");
 }

@@ -5,6 +5,10 @@
 
 namespace nrt {
 
+constexpr uint32_t QUEUE_HEADS = 8;    // one per XCD
+constexpr uint32_t QUEUE_STRIDE = 32;  // words: one 128-B line per head
+
+
 enum : uint32_t { RNG_CHACHA8 = 0, RNG_PHILOX = 1 };
 
 struct RenderParams {
@@ -27,7 +31,9 @@ struct RenderParams {
     uint32_t wave_pixels, wave_pixels_log2;
     double acc_scale, acc_unscale;  // 2^k, 2^-k
     uint32_t groups;                // Philox: pixel groups (of wave_pixels) in this launch
-    unsigned int* queue;            // Philox: group queue head (device, zeroed before the launch)
+    // Philox: QUEUE_HEADS group-queue heads, QUEUE_STRIDE words apart (device, zeroed
+    // before the launch); head x hands out the x-th contiguous eighth of the groups.
+    unsigned int* queue;
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;

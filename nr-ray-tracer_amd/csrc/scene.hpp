@@ -22,6 +22,8 @@
 #include <string>
 #include <vector>
 
+#include "noise.hpp"
+
 namespace nrt {
 
 struct V3 {
@@ -74,14 +76,14 @@ int total_cmp(double a, double b);  // f64::total_cmp as -1/0/1
 
 // ---------------------------------------------------------------- textures
 struct Texture {
-    enum Kind { Solid, Image, Checker, Unsupported } kind = Solid;
+    enum Kind { Solid, Image, Checker, Noise, Marble } kind = Solid;
     V3 color{1, 1, 1};
     // Image: Rgb32F texels (decoded u8/255, no sRGB linearisation, image.rs:76-80)
     uint32_t width = 0, height = 0;
     std::shared_ptr<std::vector<float>> texels;
     std::shared_ptr<Texture> even, odd;
     double scale = 0.5;
-    std::string note;  // Unsupported: which kind (Marble / Noise)
+    FbmParams fbm;  // Noise / Marble (noise.hpp)
 };
 using TexturePtr = std::shared_ptr<Texture>;
 

@@ -8,6 +8,7 @@
 // keeping document order.
 #include "scene_config.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <fstream>
 #include <map>
@@ -36,6 +37,11 @@ double as_f64(const Value& v, const char* what) {
 uint64_t as_usize(const Value& v, const char* what) {
     if (v.kind != Value::Int || v.i < 0) fail(std::string("invalid type for `") + what + "`: expected usize");
     return (uint64_t)v.i;
+}
+
+uint32_t as_u32(const Value& v, const char* what) {
+    if (v.kind != Value::Int || v.i < 0 || v.i > 0xFFFFFFFFll) fail(std::string("invalid type for `") + what + "`: expected u32");
+    return (uint32_t)v.i;
 }
 
 V3 as_dvec3(const Value& v, const char* what) {
@@ -146,11 +152,23 @@ TexturePtr make_texture(const Value& cfg, const TextureMap& textures) {
             t->odd = it->second;
         }
         if (auto v = opt(*body, "scale")) t->scale = as_f64(*v, "scale");
-    } else if (kind == "Marble" || kind == "Noise") {
-        // Perlin textures are outside the hot-path scope;
-        // they only fail a render that actually reaches them (flatten.cpp).
-        t->kind = Texture::Unsupported;
-        t->note = kind;
+    } else if (kind == "Marble") {
+        // MarbleBuilder::build (marble.rs:46-60): Fbm(seed), 7 octaves, frequency
+        t->kind = Texture::Marble;
+        if (auto v = opt(*body, "seed")) t->fbm.seed = as_u32(*v, "seed");
+        if (auto v = opt(*body, "frequency")) t->fbm.frequency = as_f64(*v, "frequency");
+        t->fbm.octaves = MARBLE_OCTAVES;
+    } else if (kind == "Noise") {
+        // PerlinRidgedNoiseBuilder::build (noise.rs:79-101): octaves default 1, then
+        // Fbm::set_octaves clamps to [1, 32]
+        t->kind = Texture::Noise;
+        if (auto v = opt(*body, "seed")) t->fbm.seed = as_u32(*v, "seed");
+        if (auto v = opt(*body, "frequency")) t->fbm.frequency = as_f64(*v, "frequency");
+        if (auto v = opt(*body, "lacunarity")) t->fbm.lacunarity = as_f64(*v, "lacunarity");
+        if (auto v = opt(*body, "persistence")) t->fbm.persistence = as_f64(*v, "persistence");
+        uint64_t oct = 1;
+        if (auto v = opt(*body, "octaves")) oct = as_usize(*v, "octaves");
+        t->fbm.octaves = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(oct, 1), NOISE_MAX_OCTAVES);
     } else {
         fail("unknown variant `" + kind + "` for TextureConfig");
     }

@@ -117,6 +117,7 @@ SIGNATURES = {
     "nrt_image_to_rgb8": (C.c_int, [C.POINTER(C.c_float), C.c_size_t, C.c_float, C.POINTER(C.c_uint8)]),
     "nrt_debug_rng": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                 C.POINTER(C.c_uint64)]),
+    "nrt_debug_perlin_permutation": (C.c_int, [C.c_uint32, C.POINTER(C.c_uint8)]),
     "nrt_debug_phase_profile": (C.c_int, [C.c_void_p, C.POINTER(_Camera), C.POINTER(_RenderOpts),
                                           C.POINTER(C.c_uint64), C.c_size_t]),
 }
@@ -479,4 +480,11 @@ def debug_rng(rng: str, stream0: int, lanes: int, count: int, sample: int = 0) -
     """First `count` draws of `lanes` consecutive pixel streams, computed on the GPU."""
     out = np.empty((lanes, count), dtype=np.uint64)
     _check(lib().nrt_debug_rng(RNG[rng], stream0, lanes, count, sample, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+    return out
+
+
+def debug_perlin_permutation(seed: int) -> np.ndarray:
+    """Permutation table of the Perlin source for `seed` (Noise / Marble textures), host-side."""
+    out = np.empty(256, dtype=np.uint8)
+    _check(lib().nrt_debug_perlin_permutation(seed, out.ctypes.data_as(C.POINTER(C.c_uint8))))
     return out

@@ -12,10 +12,11 @@
 //   vector.rs:27-81  objects/object.rs:40-121  objects/sphere.rs:191-285
 //   objects/plane.rs:309-460  objects/translate.rs:17-50  objects/rotate.rs:63-157
 //   objects/scale.rs:167-244  aabb.rs:13-132  interval.rs:10-94  hitable.rs:37-77
-//   materials/*.rs  textures/{solid_color,image,checker}.rs
+//   materials/*.rs  textures/{solid_color,image,checker,noise,marble}.rs
 // Third-party arithmetic restated from the pinned crates (Cargo.lock):
 //   rand_core 0.9.3 seed_from_u64 (PCG32), rand_chacha 0.9.0 ChaCha8 BlockRng,
-//   rand 0.9.2 UniformFloat::sample_single(_inclusive), glam 0.30.9 DVec3/DMat3/DMat4.
+//   rand 0.9.2 UniformFloat::sample_single(_inclusive), glam 0.30.9 DVec3/DMat3/DMat4,
+//   noise 0.9.0 Perlin/Fbm/Abs with rand 0.8.5 shuffle + rand_xorshift 0.3.0 (Perlin textures).
 // Parity pinning: the reference publishes no tests or golden vectors;
 // the ChaCha core is pinned against OpenSSL's ChaCha20 and the RFC 7539 vector
 // (tests/test_oracle.py), everything else is "parity unpinned" beyond this restatement.
@@ -25,6 +26,9 @@
 //   oracle dump <tree>                   canonical scene-graph dump (matches nrt_scene_dump)
 //   oracle rng <stream> <count>          first draws of a pixel stream (hex u64 per line)
 //   oracle chacha <rounds> <key-hex64> <ctr> <nonce> <nwords>   raw keystream words
+//   oracle xorshift <seed-hex32> <n> | perm <seed> | noise <seed> <oct> <freq> <lac> <pers> <x> <y> <z>
+//   oracle marble <seed> <freq> <x> <y> <z>      Perlin-texture pieces (tests)
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -414,6 +418,198 @@ struct Checker : Texture {
         return v % 2 == 0 ? even->get_color(uv, p) : odd->get_color(uv, p);
     }
     std::string desc() const override { return " CHECKER" + hx(scale) + " (" + even->desc() + " ) (" + odd->desc() + " )"; }
+};
+
+// ------------------------------------------------------- Perlin textures
+// textures/noise.rs:79-145 (PerlinRidgedNoise = Abs<Fbm<Perlin>>), textures/marble.rs:46-96.
+// The `noise` crate is third-party (Cargo.lock: noise 0.9.0, with rand 0.8.5 and
+// rand_xorshift 0.3.0) and absent from /root/reference: restated from its published
+// source as remembered — PARITY UNPINNED (no reference test or vector covers it).
+namespace perlin_crate {
+// rand_xorshift 0.3.0: XorShiftRng::from_seed([u8; 16]) reads 4 LE u32 (x, y, z, w)
+struct XorShiftRng {
+    uint32_t x, y, z, w;
+    explicit XorShiftRng(const uint8_t seed[16]) {
+        uint32_t v[4];
+        for (int i = 0; i < 4; ++i)
+            v[i] = (uint32_t)seed[4 * i] | (uint32_t)seed[4 * i + 1] << 8 | (uint32_t)seed[4 * i + 2] << 16 |
+                   (uint32_t)seed[4 * i + 3] << 24;
+        if (!(v[0] | v[1] | v[2] | v[3])) v[0] = v[1] = v[2] = v[3] = 0x0BAD5EEDu;
+        x = v[0]; y = v[1]; z = v[2]; w = v[3];
+    }
+    uint32_t next_u32() {
+        const uint32_t t = x ^ (x << 11);
+        x = y; y = z; z = w;
+        w = w ^ (w >> 19) ^ (t ^ (t >> 8));
+        return w;
+    }
+};
+// rand 0.8.5: Rng::gen_range(0..ubound) for u32 = UniformInt::sample_single_inclusive(0, ubound - 1)
+static uint32_t gen_range_u32(XorShiftRng& rng, uint32_t low, uint32_t high_incl) {
+    const uint32_t range = high_incl - low + 1u;
+    if (range == 0) return rng.next_u32();
+    const uint32_t zone = (range << __builtin_clz(range)) - 1u;  // "conservative but fast approximation"
+    for (;;) {
+        const uint64_t m = (uint64_t)rng.next_u32() * (uint64_t)range;  // v.wmul(range)
+        const uint32_t hi = (uint32_t)(m >> 32), lo = (uint32_t)m;
+        if (lo <= zone) return low + hi;
+    }
+}
+// noise 0.9.0 PermutationTable::new(seed): seed bytes [1,0,0,0, s0..s3 x3], Standard sample =
+// [0..=255] shuffled by SliceRandom::shuffle (for i in (1..len).rev(): swap(i, gen_index(i + 1)))
+struct PermutationTable {
+    uint8_t values[256];
+    explicit PermutationTable(uint32_t seed) {
+        uint8_t real[16] = {0};
+        real[0] = 1;
+        for (int i = 1; i < 4; ++i) {
+            real[i * 4] = (uint8_t)seed;
+            real[i * 4 + 1] = (uint8_t)(seed >> 8);
+            real[i * 4 + 2] = (uint8_t)(seed >> 16);
+            real[i * 4 + 3] = (uint8_t)(seed >> 24);
+        }
+        XorShiftRng rng(real);
+        for (int i = 0; i < 256; ++i) values[i] = (uint8_t)i;
+        for (int i = 255; i >= 1; --i) {
+            const uint32_t j = gen_range_u32(rng, 0, (uint32_t)i);
+            std::swap(values[i], values[j]);
+        }
+    }
+    // NoiseHasher::hash: fold (a & 0xff) with values[a] ^ b, then one more lookup
+    size_t hash(const int64_t* v, int n) const {
+        size_t idx = (size_t)(v[0] & 0xff);
+        for (int i = 1; i < n; ++i) idx = (size_t)values[idx] ^ (size_t)(v[i] & 0xff);
+        return values[idx];
+    }
+};
+// core/perlin.rs perlin_3d
+static double gradient_dot_v(size_t perm, double x, double y, double z) {
+    switch (perm & 0b1111) {
+        case 0: return x + y;    case 1: return -x + y;   case 2: return x - y;    case 3: return -x - y;
+        case 4: return x + z;    case 5: return -x + z;   case 6: return x - z;    case 7: return -x - z;
+        case 8: return y + z;    case 9: return -y + z;   case 10: return y - z;   case 11: return -y - z;
+        case 12: return x + y;   case 13: return -x + y;  case 14: return -y + z;  default: return -y - z;
+    }
+}
+static double map_quintic(double x) { return x * x * x * (x * (x * 6.0 - 15.0) + 10.0); }
+static double perlin_3d(const PermutationTable& hasher, DVec3 point) {
+    const double SCALE_FACTOR = 1.154'700'538'379'251'5;
+    const DVec3 floored{std::floor(point.x), std::floor(point.y), std::floor(point.z)};
+    const int64_t corner[3] = {(int64_t)floored.x, (int64_t)floored.y, (int64_t)floored.z};
+    const DVec3 distance{point.x - floored.x, point.y - floored.y, point.z - floored.z};
+    auto g = [&](int ox, int oy, int oz) {
+        const int64_t c[3] = {corner[0] + ox, corner[1] + oy, corner[2] + oz};
+        return gradient_dot_v(hasher.hash(c, 3), distance.x - (double)ox, distance.y - (double)oy,
+                              distance.z - (double)oz);
+    };
+    const double g000 = g(0, 0, 0), g100 = g(1, 0, 0), g010 = g(0, 1, 0), g110 = g(1, 1, 0);
+    const double g001 = g(0, 0, 1), g101 = g(1, 0, 1), g011 = g(0, 1, 1), g111 = g(1, 1, 1);
+    const double a = map_quintic(distance.x), b = map_quintic(distance.y), c = map_quintic(distance.z);
+    const double k0 = g000;
+    const double k1 = g100 - g000;
+    const double k2 = g010 - g000;
+    const double k3 = g001 - g000;
+    const double k4 = g000 + g110 - g100 - g010;
+    const double k5 = g000 + g101 - g100 - g001;
+    const double k6 = g000 + g011 - g010 - g001;
+    const double k7 = g100 + g010 + g001 + g111 - g000 - g110 - g101 - g011;
+    const double result = k0 + k1 * a + k2 * b + k3 * c + k4 * a * b + k5 * a * c + k6 * b * c + k7 * a * b * c;
+    return std::clamp(result * SCALE_FACTOR, -1.0, 1.0);
+}
+// f64::powi -> llvm.powi -> compiler-rt __powidf2
+static double powi(double a, int b) {
+    const bool recip = b < 0;
+    double r = 1;
+    for (;;) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1 / r : r;
+}
+// source/generators/fractals/fbm.rs
+struct Fbm {
+    static constexpr double DEFAULT_FREQUENCY = 1.0;
+    static constexpr double DEFAULT_LACUNARITY = M_PI * 2.0 / 3.0;
+    static constexpr double DEFAULT_PERSISTENCE = 0.5;
+    static constexpr size_t MAX_OCTAVES = 32;
+    uint32_t seed;
+    size_t octaves = 6;
+    double frequency = DEFAULT_FREQUENCY, lacunarity = DEFAULT_LACUNARITY, persistence = DEFAULT_PERSISTENCE;
+    std::vector<PermutationTable> sources;
+    double scale_factor;
+    static double calc_scale_factor(double persistence, size_t octaves) {
+        double denom = 0.0;
+        for (size_t x = 1; x <= octaves; ++x) denom = denom + powi(persistence, (int)x);
+        return 1.0 / denom;
+    }
+    void build_sources() {
+        sources.clear();
+        for (size_t x = 0; x < octaves; ++x) sources.emplace_back((uint32_t)(seed + (uint32_t)x));
+    }
+    explicit Fbm(uint32_t s) : seed(s) {
+        build_sources();
+        scale_factor = calc_scale_factor(persistence, octaves);
+    }
+    Fbm& set_octaves(size_t o) {
+        if (o == octaves) return *this;
+        octaves = std::clamp<size_t>(o, 1, MAX_OCTAVES);
+        build_sources();
+        scale_factor = calc_scale_factor(persistence, octaves);
+        return *this;
+    }
+    Fbm& set_frequency(double f) { frequency = f; return *this; }
+    Fbm& set_lacunarity(double l) { lacunarity = l; return *this; }
+    Fbm& set_persistence(double p) {
+        persistence = p;
+        scale_factor = calc_scale_factor(persistence, octaves);
+        return *this;
+    }
+    double get(DVec3 point) const {
+        point = point * frequency;
+        double result = 0.0;
+        for (size_t x = 0; x < octaves; ++x) {
+            double signal = perlin_3d(sources[x], point);
+            signal *= powi(persistence, (int)x);
+            result += signal;
+            point = point * lacunarity;
+        }
+        return result * scale_factor;
+    }
+};
+}  // namespace perlin_crate
+
+struct NoiseTex : Texture {  // PerlinRidgedNoise (noise.rs)
+    perlin_crate::Fbm perlin;
+    NoiseTex(uint32_t seed, size_t octaves, double frequency, double lacunarity, double persistence)
+        : perlin(seed) {
+        perlin.set_octaves(octaves).set_lacunarity(lacunarity).set_frequency(frequency).set_persistence(persistence);
+    }
+    DVec3 get_color(DVec2, DVec3 p) const override {
+        const double v = std::fabs(perlin.get(p));  // Abs
+        return v * DVec3{1.0, 1.0, 1.0};
+    }
+    std::string desc() const override {
+        char b[64];
+        snprintf(b, sizeof b, " NOISE %u %zu", perlin.seed, perlin.octaves);
+        return b + hx(perlin.frequency) + hx(perlin.lacunarity) + hx(perlin.persistence);
+    }
+};
+struct MarbleTex : Texture {  // Marble (marble.rs)
+    perlin_crate::Fbm perlin;
+    double frequency;
+    MarbleTex(uint32_t seed, double f) : perlin(seed), frequency(f) { perlin.set_octaves(7).set_frequency(f); }
+    DVec3 get_color(DVec2, DVec3 p) const override {
+        const double n = std::fabs(perlin.get(p));
+        const double v = (1. + std::sin(frequency * p.z + 10. * n)) / 2.;
+        return v * DVec3{1.0, 1.0, 1.0};
+    }
+    std::string desc() const override {
+        char b[64];
+        snprintf(b, sizeof b, " MARBLE %u %zu", perlin.seed, perlin.octaves);
+        return b + hx(perlin.frequency) + hx(perlin.lacunarity) + hx(perlin.persistence);
+    }
 };
 
 // --------------------------------------------------------------- materials
@@ -892,6 +1088,10 @@ static Scene load_tree(const std::string& path) {
                 c->odd = tex.at(U(t[4]));
                 c->scale = F(t[5]);
                 p = c;
+            } else if (t[2] == "NOISE") {  // seed octaves frequency lacunarity persistence
+                p = std::make_shared<NoiseTex>((uint32_t)U(t[3]), (size_t)U(t[4]), F(t[5]), F(t[6]), F(t[7]));
+            } else if (t[2] == "MARBLE") {  // seed frequency
+                p = std::make_shared<MarbleTex>((uint32_t)U(t[3]), F(t[4]));
             } else { fprintf(stderr, "unsupported texture %s\n", t[2].c_str()); exit(3); }
             if (tex.size() <= id) tex.resize(id + 1);
             tex[id] = p;
@@ -956,6 +1156,33 @@ int main(int argc, char** argv) {
             chacha_block(rounds, key, ctr + (uint64_t)b, nonce, out);
             for (int i = 0; i < 16 && b * 16 + i < nwords; ++i) printf("%08x\n", out[i]);
         }
+        return 0;
+    }
+    if (cmd == "xorshift" && argc == 4) {  // rand_xorshift: 16 seed bytes (hex), n x next_u32
+        uint8_t seed[16];
+        for (int i = 0; i < 16; ++i) seed[i] = (uint8_t)strtoul(std::string(argv[2]).substr((size_t)(2 * i), 2).c_str(), nullptr, 16);
+        perlin_crate::XorShiftRng r(seed);
+        for (int i = 0, n = atoi(argv[3]); i < n; ++i) printf("%u\n", r.next_u32());
+        return 0;
+    }
+    if (cmd == "perm" && argc == 3) {  // noise PermutationTable::new(seed)
+        const perlin_crate::PermutationTable t((uint32_t)strtoul(argv[2], nullptr, 10));
+        for (int i = 0; i < 256; ++i) printf("%u%c", t.values[i], i == 255 ? '\n' : ' ');
+        return 0;
+    }
+    if ((cmd == "noise" && argc == 10) || (cmd == "marble" && argc == 7)) {  // texture value at a point (%a)
+        TexP t;
+        int k = 2;
+        if (cmd == "noise") {
+            t = std::make_shared<NoiseTex>((uint32_t)strtoul(argv[2], nullptr, 10), (size_t)strtoull(argv[3], nullptr, 10),
+                                           strtod(argv[4], nullptr), strtod(argv[5], nullptr), strtod(argv[6], nullptr));
+            k = 7;
+        } else {
+            t = std::make_shared<MarbleTex>((uint32_t)strtoul(argv[2], nullptr, 10), strtod(argv[3], nullptr));
+            k = 4;
+        }
+        const DVec3 c = t->get_color({0, 0}, {strtod(argv[k], nullptr), strtod(argv[k + 1], nullptr), strtod(argv[k + 2], nullptr)});
+        printf("%a\n", c.x);
         return 0;
     }
     if (cmd == "rng" && argc == 4) {

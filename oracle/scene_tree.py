@@ -9,6 +9,7 @@ so comparing the two (tests/test_loader_parity.py) checks the product loader.
 Tree format (one item per line, floats as float.hex()):
     CAMERA W H spp bounces bg3 look_from3 look_at3 view_up3 defocus_rad focus fov_rad
     TEX id SOLID r g b | TEX id IMAGE w h <raw f32 file> | TEX id CHECKER even odd scale
+    TEX id NOISE seed octaves frequency lacunarity persistence | TEX id MARBLE seed frequency
     MAT id LAMBERTIAN tex | METAL fuzz tex | DIELECTRIC ri | DIFFUSE_LIGHT intensity tex
     OBJ id SPHERE c3 r mat | QUAD p3 u3 v3 mat | TRIANGLE p3 u3 v3 mat
     OBJ id BVH n child... | TRANSLATE child o3 | ROTATE x|y|z child angle | SCALE child s3
@@ -130,6 +131,12 @@ def _usize(v: Any, what: str) -> int:
     return v
 
 
+def _u32(v: Any, what: str) -> int:
+    if isinstance(v, bool) or not isinstance(v, int) or not 0 <= v <= 0xFFFFFFFF:
+        raise LoadError(f"invalid type for `{what}`: expected u32")
+    return v
+
+
 def _vec3(v: Any, what: str) -> tuple:
     if not isinstance(v, list) or len(v) != 3:
         raise LoadError(f"invalid value for `{what}`")
@@ -244,8 +251,17 @@ class Builder:
                 odd = textures[b["odd"]]
             scale = _num(b["scale"], "scale") if b.get("scale") is not None else 0.5
             return self.w.tex(f"CHECKER {even} {odd} {_f(scale)}")
-        if kind in ("Marble", "Noise"):
-            return -1  # out of scope: only an error if a rendered material uses it
+        if kind == "Marble":  # MarbleBuilder (marble.rs:46-60); the oracle applies octaves = 7
+            seed = _u32(b["seed"], "seed") if b.get("seed") is not None else 0
+            freq = _num(b["frequency"], "frequency") if b.get("frequency") is not None else 1.0
+            return self.w.tex(f"MARBLE {seed} {_f(freq)}")
+        if kind == "Noise":  # PerlinRidgedNoiseBuilder (noise.rs:79-101): builder defaults, Fbm clamps
+            seed = _u32(b["seed"], "seed") if b.get("seed") is not None else 0
+            octaves = _usize(b["octaves"], "octaves") if b.get("octaves") is not None else 1
+            freq = _num(b["frequency"], "frequency") if b.get("frequency") is not None else 1.0
+            lac = _num(b["lacunarity"], "lacunarity") if b.get("lacunarity") is not None else math.pi * 2.0 / 3.0
+            pers = _num(b["persistence"], "persistence") if b.get("persistence") is not None else 0.5
+            return self.w.tex(f"NOISE {seed} {octaves} {_f(freq)} {_f(lac)} {_f(pers)}")
         raise LoadError(f"unknown variant `{kind}`")
 
     @staticmethod
@@ -376,8 +392,6 @@ def build_tree(path: str, overrides: CameraConfig | None, texel_dir: str) -> tup
     head = ("CAMERA {} {} {} {} ".format(cam.width, cam.height, cam.samples_per_pixel, cam.ray_max_bounces)
             + " ".join(_f(x) for x in (*cam.background_color, *cam.look_from, *cam.look_at, *cam.view_up))
             + f" {_f(cam.defocus_angle)} {_f(cam.focus_dist)} {_f(cam.field_of_view)}")
-    if any(" -1" == ln[-3:] and ln.startswith("MAT") for ln in w.lines):
-        raise LoadError("a material uses a Perlin texture (out of scope)")
     return "\n".join([head, *w.lines, f"ROOT {root}"]) + "\n", cam
 
 

@@ -31,6 +31,8 @@ CASES_F64 = [
     ("scenes/cornell-box-scene.json", 20, 20, 3, 2),      # bounce cap 2 (Q6)
     ("scenes/utah-teapot-scene.json", 32, 24, 2, None),   # 7520 triangles, deep BLAS (generated model, Q16)
     ("scenes/earth.toml", 48, 27, 2, None),               # image textures (JPEG), r = 1000 ground sphere
+    ("scenes/noise.toml", 40, 30, 2, None),               # Perlin Noise + Marble textures (parity unpinned)
+    ("scenes/simple-lights.toml", 40, 30, 2, None),       # Marble + emissive quad / sphere
 ]
 
 
@@ -123,7 +125,7 @@ def test_row_interleave_is_bitwise_identical():
 
 STAT_CASES = [("scenes/cornell-box-scene.json", 48, 48, 64), ("scenes/spheres.toml", 64, 36, 32),
               ("scenes/cube-scene.json", 40, 30, 32), ("scenes/utah-teapot-scene.json", 32, 24, 32),
-              ("scenes/earth.toml", 48, 27, 32)]
+              ("scenes/earth.toml", 48, 27, 32), ("scenes/noise.toml", 40, 30, 32)]
 
 
 @pytest.mark.parametrize("precision,rng,trace", [("f32", "chacha8", "auto"), ("f32", "philox", "auto"),

@@ -25,6 +25,8 @@ LOADABLE = [
     ("scenes/cube-model.toml", dict(width=8, height=8)),
     ("scenes/utah-teapot-scene.json", dict(width=64, height=64, spp=4)),  # generated model (Q16)
     ("scenes/earth.toml", dict(width=64, height=36, spp=2)),              # two 2048x1024 JPEG textures
+    ("scenes/noise.toml", dict(width=40, height=30, spp=2)),              # Perlin Noise + Marble textures
+    ("scenes/simple-lights.toml", dict(width=40, height=30, spp=2)),      # Marble + lights
 ]
 
 
@@ -94,8 +96,6 @@ def test_spheres_counts():
 
 @pytest.mark.parametrize("scene,code", [
     ("scenes/triangles.toml", -2),           # legacy schema (Q14)
-    ("scenes/noise.toml", -4),               # Perlin textures: outside the accelerated path
-    ("scenes/simple-lights.toml", -4),
     ("scenes/does-not-exist.json", -2),
     ("scenes/textures/earth.jpg", -2),       # not a scene format
 ])
