@@ -176,6 +176,18 @@ struct ChaCha8 {
     }
 };
 
+// a ^ b ^ k as one v_xor3_b32 with the round key in an SGPR (gfx950 VOP3 takes no
+// literal, so a constant key would cost a second v_xor_b32 per output word)
+__device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
+#if NRT_XOR3_KEY
+    uint32_t r;
+    asm("v_xor3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 // Philox4x32-10 (Salmon et al. 2011), counter = (pixel, sample, pair, 0), key = (0, 0).
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                               uint32_t k1, uint32_t out[4]) {
@@ -186,7 +198,8 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        const uint32_t n0 = r > 0 ? xor3_key(hi1, c1, k0) : hi1 ^ c1 ^ k0;
+        const uint32_t n2 = r > 0 ? xor3_key(hi0, c3, k1) : hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
@@ -554,7 +567,7 @@ __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t
     }
 }
 
-template <typename R, int MAXD>
+template <typename R, int MAXD, bool FLAT = false>
 __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 4, "world-space mode is an f32-kernel mode");
     const ConstPrimWorld<float> wp = (ConstPrimWorld<float>)sc.wprims;
@@ -637,7 +650,7 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
             }
             continue;
         }
-        if (kind == PRIM_SPHERE) {
+        if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres (not compiled in)
             for (; k < end; ++k) {
                 DPrim<R> sp;
                 for (int c = 0; c < 3; ++c) { sp.a[c] = wp[k].N[c]; sp.b[c] = wp[k].AB[c]; }
@@ -994,10 +1007,10 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
     return found;
 }
 
-template <typename R, int MAXD, bool EXACT>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       int32_t* stack) {
-    if constexpr (MAXD == 0) return trace_world(sc, wray, hm);
+    if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh(sc, wray, hm, stack);
     else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
@@ -1006,7 +1019,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
 // World-space record (MAXD <= 0; device_scene.hpp DPrimWorld): the
 // reference's front-face sign signum(d'.n) = signum(d.(M^T n)), shading normal
 // mapped out by the chain's rotations only.
-template <typename R, int MAXD>
+template <typename R, int MAXD, bool FLAT = false>
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
     // hm.prim is always a primitive record: box and room hits name their face quad
@@ -1016,7 +1029,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     Rec<R> h;
     h.p = pw;
     V<R> geo, shade;
-    if (kind == PRIM_SPHERE) {
+    if (!FLAT && kind == PRIM_SPHERE) {
         const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
         geo = normalize(h.p - center);
         shade = geo;
@@ -1110,9 +1123,9 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     return h;
 }
 
-template <typename R, int MAXD, bool EXACT>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false>
 __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
-    if constexpr (MAXD <= 0) return make_record_world(sc, wray, hm);
+    if constexpr (MAXD <= 0) return make_record_world<R, MAXD, FLAT>(sc, wray, hm);
     else return make_record_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
@@ -1294,15 +1307,17 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 //
 // Kernel variant flags: KF_PROF = phase-profile stamps (diagnostics), KF_PERLIN = the
 // scene has Noise / Marble textures (their f64 Fbm code is only compiled into the
-// variants that need it: it would raise the register budget of every other scene).
-constexpr int KF_PROF = 1, KF_PERLIN = 2;
+// variants that need it: it would raise the register budget of every other scene),
+// KF_FLAT = world-list scene without spheres whose materials all have solid colours
+// (no f64 sphere test, uv mapping or texture lookup compiled in: the Cornell box).
+constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4;
 
 template <typename R, class G, int MAXD>
-constexpr int min_waves_per_simd(bool perlin = false) {
+constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WORLD_LIST_WAVES
 #define NRT_WORLD_LIST_WAVES 6
 #endif
-    return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !perlin) ? NRT_WORLD_LIST_WAVES : 1;
+    return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
 }
 static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole waves");
 
@@ -1323,10 +1338,12 @@ struct MatV {
 };
 
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0>
-__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>((KFLAGS & KF_PERLIN) != 0)))
+__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>(KFLAGS)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     constexpr bool PROF = (KFLAGS & KF_PROF) != 0;
     constexpr bool PERLIN = (KFLAGS & KF_PERLIN) != 0;
+    constexpr bool FLAT = (KFLAGS & KF_FLAT) != 0;
+    static_assert(!FLAT || (MAXD == 0 && !PERLIN), "KF_FLAT is a world-list variant");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
     // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
@@ -1370,7 +1387,10 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     V<R> tp = mk(R(1), R(1), R(1));
     uint4 w = make_uint4(0u, 0u, 0u, 0u);  // Philox: this segment's block
 
-    auto albedo = [&](const MatV<R>& m, const Rec<R>& h) { return m.solid ? m.color : tex_color<R, PERLIN>(sc, m.tex, h.u, h.v, h.p); };
+    auto albedo = [&](const MatV<R>& m, const Rec<R>& h) {
+        if constexpr (FLAT) return m.color;  // every texture is a SolidColor
+        else return m.solid ? m.color : tex_color<R, PERLIN>(sc, m.tex, h.u, h.v, h.p);
+    };
 
     auto material = [&](uint32_t mat) {  // the material table is LDS-resident: re-reading is cheap
         MatV<R> m;
@@ -1403,7 +1423,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             contrib = tp * background;
             return false;
         }
-        h = make_record<R, MAXD, EXACT>(sc, ray, hm);
+        h = make_record<R, MAXD, EXACT, FLAT>(sc, ray, hm);
         m = material(h.mat);
         if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
             const R k = bounced ? m.param : R(1.0);
@@ -1568,7 +1588,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
-                    hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);
@@ -1743,7 +1763,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 sh = alive;
                 traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
                 // world list: the global tables through the scalar cache; records read LDS
-                if (traced) hit = trace<R, MAXD, EXACT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                if (traced) hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
             }
             const unsigned long long t1 = stamp();
             Rec<R> h;

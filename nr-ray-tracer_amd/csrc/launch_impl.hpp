@@ -57,14 +57,30 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
 }
 
 template <typename R, class G, int MAXD, bool EXACT>
-static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perlin, hipStream_t stream) {
+static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perlin, hipStream_t stream,
+                       bool flat = false) {
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
                           (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v);
+    using dev::KF_FLAT;
     using dev::KF_PERLIN;
     using dev::KF_PROF;
+    constexpr bool FLAT_MODE = MAXD == 0 && sizeof(R) == 4;  // KF_FLAT exists for the f32 world list only
+    if constexpr (FLAT_MODE) {
+        if (flat && !perlin) {  // the phase profile measures this same variant
+            if (p.counters) {
+                if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, KF_PROF | KF_FLAT>(p, v, ring + scene, stream);
+                else launch_variant<R, G, MAXD, EXACT, false, KF_PROF | KF_FLAT>(p, v, ring, stream);
+            } else if (scene <= LDS_SCENE_LIMIT) {
+                launch_variant<R, G, MAXD, EXACT, true, KF_FLAT>(p, v, ring + scene, stream);
+            } else {
+                launch_variant<R, G, MAXD, EXACT, false, KF_FLAT>(p, v, ring, stream);
+            }
+            return;
+        }
+    }
     if (p.counters) {  // diagnostic phase profile (nrt_debug_phase_profile)
         if constexpr (MAXD > 1) {
             throw std::runtime_error("phase profile: flat-instance scenes only");

@@ -48,6 +48,7 @@ struct DeviceScene {
     uint64_t world_units = 0;
     bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
     bool perlin = false;    // Noise / Marble textures present (KF_PERLIN kernel variants)
+    bool flat = false;      // world list without spheres, solid colours only (KF_FLAT variants)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
     // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS sets of
@@ -117,6 +118,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.wbvh.nodes.size()};
         ds->wbvh_ok = fs.wbvh_ok;
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
+        ds->flat = !ds->perlin;
+        for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
+        for (const DPrimWorld<float>& q : f32.wprims) ds->flat &= (q.meta & WKIND_MASK) != PRIM_SPHERE;
         ds->wbvh_prims = wbp;
         const size_t qbytes = (size_t)QUEUE_SLOTS * QUEUE_HEADS * QUEUE_STRIDE * sizeof(unsigned int);
         check(hipMalloc((void**)&ds->queues, qbytes), "hipMalloc(queues)");
@@ -191,7 +195,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         } else {
             v.n_wprims = 0;
         }
-        launch_fast(q, v, rng, maxd, ds->perlin, stream);
+        launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
     }
     check(hipGetLastError(), "render kernel launch");
 }
