@@ -91,6 +91,31 @@ def load_pmc(precision, rng):
         return {}
 
 
+def load_work(scene, w, h):
+    """Per-sample algorithmic work of this config (tests/golden/work_counts.json), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "work_counts.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        wc = json.load(fh)
+    for name, c in wc["configs"].items():
+        if c["scene"] == scene and c["width"] == w and c["height"] == h:
+            return dict(c, name=name)
+    return None
+
+
+def work_block(wc, msamples_per_s, precision):
+    """rays/s and the algorithmic VALU-FLOP fraction (oracle event counts x SURVEY §8(d) costs)."""
+    if wc is None:
+        return None
+    tflops = wc["flops_per_sample"] * msamples_per_s * 1e6 / 1e12
+    return {"rays_per_s": round(wc["rays_per_sample"] * msamples_per_s * 1e6, 1),
+            "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"],
+            "algorithmic_tflops": round(tflops, 3), "valu_peak_tflops": VALU_PEAK_TFLOPS[precision],
+            "valu_flop_frac": round(tflops / VALU_PEAK_TFLOPS[precision], 4),
+            "source": f"tests/golden/work_counts.json[{wc['name']}] (oracle event counts, ChaCha8 stream)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,6 +228,7 @@ def main():
                          "valu_issue_frac": pmc.get("valu_issue_frac"),
                          "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                          "pmc_source": "profiles/pmc_summary.json" if pmc else None},
+            "work": work_block(load_work(args.scene, W, H), value, args.precision),
             "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4)},
         }
         if not args.no_cpu_baseline and world == 1:

@@ -1,0 +1,49 @@
+"""tests/golden/work_counts.json (SURVEY §8(d) algorithmic work per sample) is what the
+counting oracle produces: C1 is sampled in full (every pixel, full spp), so its counts
+are deterministic and re-derived exactly here; every config's FLOP figure is the sum
+of its event rates times the committed costs."""
+import json
+import os
+import sys
+
+import pytest
+
+from helpers import GOLDEN, ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def _load():
+    with open(os.path.join(GOLDEN, "work_counts.json")) as fh:
+        return json.load(fh)
+
+
+def test_flops_are_rates_times_costs():
+    wc = _load()
+    for name, c in wc["configs"].items():
+        flops = sum(c["per_sample"][k] * cost for k, cost in wc["costs"].items())
+        assert flops == pytest.approx(c["flops_per_sample"], rel=1e-5), name
+        assert c["rays_per_sample"] >= 1.0, name  # every sample traces its camera ray
+
+
+def test_c1_counts_rederived():
+    import work_counts
+
+    wc = _load()
+    scene, w, h, _, spp, stride = work_counts.CONFIGS["C1"]
+    assert stride == 1 and spp == wc["configs"]["C1"]["full_spp"]
+    r = work_counts.count(scene, w, h, spp, stride)
+    assert r["samples"] == wc["configs"]["C1"]["samples"]
+    assert r["per_sample"] == wc["configs"]["C1"]["per_sample"]
+
+
+def test_bench_work_block():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    c5 = bench.load_work(bench.DEFAULT_SCENE, 1024, 1024)
+    assert c5["name"] == "C5"
+    blk = bench.work_block(c5, 1000.0, "f32")
+    assert blk["rays_per_s"] == pytest.approx(c5["rays_per_sample"] * 1e9, rel=1e-6)
+    assert 0 < blk["valu_flop_frac"] < 1
+    assert bench.load_work(bench.DEFAULT_SCENE, 100, 100) is None
