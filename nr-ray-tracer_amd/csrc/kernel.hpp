@@ -176,18 +176,6 @@ struct ChaCha8 {
     }
 };
 
-// a ^ b ^ k as one v_xor3_b32 with the round key in an SGPR (gfx950 VOP3 takes no
-// literal, so a constant key would cost a second v_xor_b32 per output word)
-__device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
-#if NRT_XOR3_KEY
-    uint32_t r;
-    asm("v_xor3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-    return r;
-#else
-    return a ^ b ^ k;
-#endif
-}
-
 // Philox4x32-10 (Salmon et al. 2011), counter = (pixel, sample, pair, 0), key = (0, 0).
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                               uint32_t k1, uint32_t out[4]) {
@@ -198,8 +186,7 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        const uint32_t n0 = r > 0 ? xor3_key(hi1, c1, k0) : hi1 ^ c1 ^ k0;
-        const uint32_t n2 = r > 0 ? xor3_key(hi0, c3, k1) : hi0 ^ c3 ^ k1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
