@@ -29,7 +29,7 @@ struct FlatScene {
     // World-space primitives in the reference's depth-first candidate order
     // (device_scene.hpp DPrimWorld); world_ok = every primitive qualifies.
     std::vector<DPrimWorld<double>> wprims;
-    std::vector<uint32_t> wruns;  // kind | count << 2 over wprims
+    std::vector<uint32_t> wruns;  // kind | count << WKIND_BITS over world units
     uint64_t world_units = 0;     // primitives + fused boxes: the world list's test count
     uint32_t wflags = 0;          // WFLAG_* of the world list
     bool world_ok = false;

@@ -1304,6 +1304,10 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WORLD_LIST_WAVES
 #define NRT_WORLD_LIST_WAVES 6
 #endif
+#ifndef NRT_FLAT_WAVES
+#define NRT_FLAT_WAVES NRT_WORLD_LIST_WAVES
+#endif
+    if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT)) return NRT_FLAT_WAVES;
     return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
 }
 static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole waves");

@@ -120,7 +120,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->flat = !ds->perlin;
         for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
-        for (const DPrimWorld<float>& q : f32.wprims) ds->flat &= (q.meta & WKIND_MASK) != PRIM_SPHERE;
+        // unit kinds from the runs (box / room units also hold header and empty face slots)
+        for (uint32_t run : fs.wruns) ds->flat &= (run & WKIND_MASK) != PRIM_SPHERE;
+        ds->flat &= !fs.wruns.empty();
         ds->wbvh_prims = wbp;
         const size_t qbytes = (size_t)QUEUE_SLOTS * QUEUE_HEADS * QUEUE_STRIDE * sizeof(unsigned int);
         check(hipMalloc((void**)&ds->queues, qbytes), "hipMalloc(queues)");
