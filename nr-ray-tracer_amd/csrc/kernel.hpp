@@ -177,16 +177,50 @@ struct ChaCha8 {
 };
 
 // Philox4x32-10 (Salmon et al. 2011), counter = (pixel, sample, pair, 0), key = (0, 0).
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1, uint32_t out[4]) {
+// Rounds 1-9 mix the round key into one word with one v_bitop3_b32 (hi ^ c ^ key):
+// VOP3 takes no literal on gfx950, so the round keys live in two SGPRs stepped by
+// the scalar unit (volatile: the compiler neither folds them into per-round literals,
+// which would cost a second v_xor_b32 per word, nor hoists ten keys into SGPRs).
+#ifndef NRT_PHILOX_SKEY
+#ifdef __HIP_DEVICE_COMPILE__  // (the host pass of the TU has no SGPR / VGPR constraints)
+#define NRT_PHILOX_SKEY 1
+#else
+#define NRT_PHILOX_SKEY 0
+#endif
+#endif
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+#if NRT_PHILOX_SKEY
+    uint32_t k0, k1;
+    asm volatile("s_mov_b32 %0, 0x9e3779b9" : "=s"(k0));
+    asm volatile("s_mov_b32 %0, 0xbb67ae85" : "=s"(k1));
+#else
+    uint32_t k0 = 0u, k1 = 0u;
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         // one widening multiply each (v_mad_u64_u32) instead of separate lo / hi multiplies
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        uint32_t n0, n2;
+#if NRT_PHILOX_SKEY
+        if (r == 0) {  // key (0, 0)
+            n0 = hi1 ^ c1;
+            n2 = hi0 ^ c3;
+        } else {
+            if (r > 1) {
+                asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(k0) : : "scc");
+                asm volatile("s_add_u32 %0, %0, 0xbb67ae85" : "+s"(k1) : : "scc");
+            }
+            // bitop3 table 0x96 = a ^ b ^ c (the compiler does not form it on its own)
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+        }
+#else
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        n0 = hi1 ^ c1 ^ k0;
+        n2 = hi0 ^ c3 ^ k1;
+#endif
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
@@ -212,7 +246,7 @@ struct Philox {
     __device__ __forceinline__ uint32_t next32() {
         if (left == 0) {
             uint32_t w[4];
-            philox4x32_10(pix, sample, pair, 0u, 0u, 0u, w);
+            philox4x32_10(pix, sample, pair, 0u, w);
             ++pair;
             w0 = w[0]; w1 = w[1]; w2 = w[2]; w3 = w[3];
             left = 4;
@@ -231,7 +265,7 @@ struct Philox {
     __device__ __forceinline__ uint4 block(uint32_t smp, uint32_t step) const { return block_at(pix, smp, step); }
     static __device__ __forceinline__ uint4 block_at(uint32_t pixel, uint32_t smp, uint32_t step) {
         uint32_t w[4];
-        philox4x32_10(pixel, smp, step, 0u, 0u, 0u, w);
+        philox4x32_10(pixel, smp, step, 0u, w);
         return make_uint4(w[0], w[1], w[2], w[3]);
     }
 };
