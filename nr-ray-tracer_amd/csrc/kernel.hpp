@@ -712,9 +712,10 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
 // lane's stack (LDS, entry k at stack[k * BLOCK]), so t_best shrinks early and
 // culls the far side.  The lanes of a wave descend until each holds a leaf (or
 // is done) before leaves are tested together ("while-while").
+template <bool FLAT = false>
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
     const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
-    if (kind == PRIM_SPHERE) {
+    if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres
         DPrim<float> sp;
         for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
         sp.s = q.D;
@@ -770,12 +771,12 @@ __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray
 }
 
 // Test the primitives of leaf `ref` (world_prim_t, closest hit so far in ts).
-template <typename R>
+template <typename R, bool FLAT>
 __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
     const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
     for (uint32_t k = 0; k < cnt; ++k) {
         const DPrimWorld<float> q = load16(sc.wprims + first + k);
-        const float t = world_prim_t(q, ray, ts.t_best);
+        const float t = world_prim_t<FLAT>(q, ray, ts.t_best);
         const bool ok = t >= 0.0f;
         ts.t_best = ok ? t : ts.t_best;
         ts.best = ok ? (int32_t)(first + k) : ts.best;
@@ -856,7 +857,7 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
 // done), lanes waiting for the wave's slowest; then test the leaf.  With
 // NRT_SPECULATIVE (Aila & Laine) a lane that meets a leaf parks it and keeps
 // descending until every lane of the wave has a leaf.
-template <typename R, bool WIDE>
+template <typename R, bool WIDE, bool FLAT>
 __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
                                                 int32_t* stack) {
 #if NRT_SPECULATIVE
@@ -874,7 +875,7 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
         }
     }
     if (ts.leaf != WBVH_NO_LEAF) {
-        wbvh_leaf(ts, sc, ray, ts.leaf);
+        wbvh_leaf<R, FLAT>(ts, sc, ray, ts.leaf);
         ts.leaf = WBVH_NO_LEAF;
     }
 #else
@@ -883,20 +884,20 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
         else wbvh2_visit(ts, sc, stack);
     }
     if (ts.node == WBVH_DONE) return;
-    wbvh_leaf(ts, sc, ray, ts.node);
+    wbvh_leaf<R, FLAT>(ts, sc, ray, ts.node);
     ts.node = wbvh_pop(ts, stack);
 #endif
 }
 
-template <typename R>
+template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
                                            int32_t* stack) {
-    wbvh_round_impl<R, false>(ts, sc, ray, stack);
+    wbvh_round_impl<R, false, FLAT>(ts, sc, ray, stack);
 }
-template <typename R>
+template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh4_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
                                             int32_t* stack) {
-    wbvh_round_impl<R, true>(ts, sc, ray, stack);
+    wbvh_round_impl<R, true, FLAT>(ts, sc, ray, stack);
 }
 
 // Root and round of the tree the scene carries (4-wide when its stack bound fits).
@@ -904,19 +905,19 @@ template <typename R>
 __device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
     return sc.wbvh4 ? sc.wbvh4_root : sc.wbvh_root;
 }
-template <typename R>
+template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack) {
-    if (sc.wbvh4) wbvh4_round(ts, sc, ray, stack);
-    else wbvh_round(ts, sc, ray, stack);
+    if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack);
+    else wbvh_round<R, FLAT>(ts, sc, ray, stack);
 }
 
-template <typename R, int MAXD>
+template <typename R, int MAXD, bool FLAT = false>
 __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm,
                                                 int32_t* stack) {
     static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), ray);
-    while (ts.busy()) wbvh_step(ts, sc, ray, stack);
+    while (ts.busy()) wbvh_step<R, FLAT>(ts, sc, ray, stack);
     hm.t = ts.t_best;
     hm.prim = (uint32_t)ts.best;
     hm.depth = 0;
@@ -1032,7 +1033,7 @@ template <typename R, int MAXD, bool EXACT, bool FLAT = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       int32_t* stack) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
-    else if constexpr (MAXD < 0) return trace_world_bvh(sc, wray, hm, stack);
+    else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
@@ -1368,7 +1369,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     constexpr bool PROF = (KFLAGS & KF_PROF) != 0;
     constexpr bool PERLIN = (KFLAGS & KF_PERLIN) != 0;
     constexpr bool FLAT = (KFLAGS & KF_FLAT) != 0;
-    static_assert(!FLAT || (MAXD == 0 && !PERLIN), "KF_FLAT is a world-list variant");
+    static_assert(!FLAT || (MAXD <= 0 && !PERLIN), "KF_FLAT is a world-list / world-BVH variant");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
     // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
@@ -1577,7 +1578,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = active && ts.busy();
                     if (__ballot(going) == 0ull) break;
                     if ((uint32_t)__popcll(__ballot(active && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step(ts, gsc, ray, stack);
+                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack);
                 }
                 const unsigned long long t1 = stamp();
                 if (active && !ts.busy()) {
@@ -1776,7 +1777,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = alive && ts.busy();
                     if (__ballot(going) == 0ull) break;
                     if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step(ts, gsc, ray, stack);
+                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack);
                 }
                 sh = alive && !ts.busy();
                 traced = sh && !killed && b < p.max_bounces;

@@ -9,7 +9,7 @@ namespace nrt {
 template <class G>
 static void launch_fast_rng(const RenderParams& p, const DSceneView<float>& v, int maxd, bool perlin, bool flat,
                             hipStream_t stream) {
-    if (maxd == MODE_WORLD_BVH) launch_one<float, G, MODE_WORLD_BVH, false>(p, v, perlin, stream);
+    if (maxd == MODE_WORLD_BVH) launch_one<float, G, MODE_WORLD_BVH, false>(p, v, perlin, stream, flat);
     else if (maxd == MODE_WORLD_LIST) launch_one<float, G, MODE_WORLD_LIST, false>(p, v, perlin, stream, flat);
     else if (maxd == 1) launch_one<float, G, 1, false>(p, v, perlin, stream);
     else launch_one<float, G, MAX_INSTANCE_DEPTH, false>(p, v, perlin, stream);

@@ -17,7 +17,7 @@ namespace nrt {
 constexpr int MODE_WORLD_LIST = 0;
 constexpr int MODE_WORLD_BVH = -1;
 // perlin: the scene has Noise / Marble textures (selects the KF_PERLIN kernel variants);
-// flat: no spheres and only solid-colour textures (the KF_FLAT world-list variants)
+// flat: no spheres and only solid-colour textures (the KF_FLAT world-list / world-BVH variants)
 void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, int maxd, bool perlin,
                   hipStream_t stream);
 void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, int maxd, bool perlin, bool flat,

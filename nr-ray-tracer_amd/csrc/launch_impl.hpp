@@ -67,7 +67,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     using dev::KF_FLAT;
     using dev::KF_PERLIN;
     using dev::KF_PROF;
-    constexpr bool FLAT_MODE = MAXD == 0 && sizeof(R) == 4;  // KF_FLAT exists for the f32 world list only
+    constexpr bool FLAT_MODE = MAXD <= 0 && sizeof(R) == 4;  // KF_FLAT: f32 world list / world BVH
     if constexpr (FLAT_MODE) {
         if (flat && !perlin) {  // the phase profile measures this same variant
             if (p.counters) {
