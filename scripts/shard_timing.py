@@ -1,0 +1,38 @@
+"""Strong-scaling headroom of the render kernel on one GPU: kernel time of rank 0's
+row shard (rows y = 0 mod N) for N = 1, 2, 4, 8, against 1/N of the full frame.
+
+usage: python scripts/shard_timing.py [scene] [W H spp]
+"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nr-ray-tracer_amd"))
+import nrt  # noqa: E402
+
+scene = sys.argv[1] if len(sys.argv) > 1 else "scenes/cornell-box-scene.json"
+W, H, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1024, 1024, 256)
+os.chdir(os.path.join(ROOT, "tests", "golden"))
+s = nrt.Scene.load(scene, nrt.CameraConfig(width=W, height=H, samples_per_pixel=spp))
+s.upload(0)
+buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
+stream = torch.cuda.current_stream()
+res = {}
+for n in (1, 2, 4, 8):
+    rows = (H + n - 1) // n
+    times = []
+    for it in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        s.render_device(buf.data_ptr(), rows * W * 3, row_offset=0, row_stride=n, stream=stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if it:
+            times.append(e0.elapsed_time(e1))
+    res[n] = sum(times) / len(times)
+out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(res[1] / (n * t), 4)} for n, t in res.items()}
+out["env"] = {k: v for k, v in os.environ.items() if k.startswith("NRT_")}
+print(json.dumps(out))
