@@ -10,4 +10,5 @@ bash scripts/round_profile.sh ${tag} > gpurun_out/${tag}_round_profile.log 2>&1 
 tail -1 gpurun_out/${tag}_round_profile.log
 bash scripts/configs_bench.sh ${tag}_cfg || exit 1
 timeout -k 10 200 python scripts/phase_profile.py scenes/cornell-box-scene.json f32/philox/auto f32/chacha8/auto > gpurun_out/${tag}_phase.json 2>/dev/null || exit 1
+timeout -k 10 120 python scripts/shard_timing.py > gpurun_out/${tag}_shard_c5.json 2>/dev/null || exit 1
 echo done
