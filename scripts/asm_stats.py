@@ -18,7 +18,7 @@ def main():
     frag = args.pop(0) if args and not args[0].startswith("-") else "PhiloxELi0ELb0ELb1ELi4EE"
     pkg = os.path.join(ROOT, "nr-ray-tracer_amd")
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "-fPIC", "-fno-fast-math", "-Wno-unused-function", "-Icsrc",
-           "-I../include", "-x", "hip", "--offload-arch=gfx950", "-ffp-contract=fast", "--cuda-device-only", "-S",
+           "-I../include", "-x", "hip", "--offload-arch=gfx950", "-ffp-contract=fast", "-mllvm", "-amdgpu-use-amdgpu-trackers", "--cuda-device-only", "-S",
            "csrc/kernels_fast.hip", "-o", "/tmp/nrt_all.s"] + args
     subprocess.run(cmd, cwd=pkg, check=True, capture_output=True)
     s = open("/tmp/nrt_all.s").read()
