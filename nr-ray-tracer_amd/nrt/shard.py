@@ -28,17 +28,29 @@ def assemble(gathered: List["torch.Tensor"], height: int) -> "torch.Tensor":
     return torch.stack(gathered, 0).transpose(0, 1).reshape(rmax * world, width, 3)[:height]
 
 
+_staging = {}
+
+
 def gather_frame(buf: "torch.Tensor", height: int, dist, rank: int, world: int, out=None):
     """The single collective of a step: dist.gather of every rank's row buffer to rank 0,
-    then the un-permute into `out` (rank 0).  Returns the frame on rank 0, None elsewhere."""
+    straight into slices of one cached (N, rows_max, W, 3) staging tensor, then the
+    un-permute into `out` (rank 0) as one strided copy.  Returns the frame on rank 0,
+    None elsewhere."""
     import torch
 
-    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, gather_list=parts, dst=0)
     if rank != 0:
+        dist.gather(buf, gather_list=None, dst=0)
         return None
-    frame = assemble(parts, height)
+    key = (buf.device, buf.dtype, world, tuple(buf.shape))
+    stage = _staging.get(key)
+    if stage is None:
+        stage = _staging[key] = torch.empty((world,) + tuple(buf.shape), dtype=buf.dtype, device=buf.device)
+    dist.gather(buf, gather_list=list(stage.unbind(0)), dst=0)
+    rmax, width = buf.shape[0], buf.shape[1]
     if out is None:
-        return frame.contiguous()
-    out.copy_(frame)
+        return assemble(list(stage.unbind(0)), height).contiguous()
+    if rmax * world == height:  # row y = compact row y // N of rank y % N
+        out.view(rmax, world, width, 3).copy_(stage.transpose(0, 1))
+    else:
+        out.copy_(stage.transpose(0, 1).reshape(rmax * world, width, 3)[:height])
     return out
