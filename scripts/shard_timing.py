@@ -1,7 +1,7 @@
 """Strong-scaling headroom of the render kernel on one GPU: kernel time of rank 0's
 row shard (rows y = 0 mod N) for N = 1, 2, 4, 8, against 1/N of the full frame.
 
-usage: python scripts/shard_timing.py [scene] [W H spp]
+usage: python scripts/shard_timing.py [scene] [W H spp] [N,N,...]
 """
 import json
 import os
@@ -21,7 +21,8 @@ s.upload(0)
 buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
 stream = torch.cuda.current_stream()
 res = {}
-for n in (1, 2, 4, 8):
+ns = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1, 2, 4, 8]
+for n in ns:
     rows = (H + n - 1) // n
     times = []
     for it in range(4):
@@ -33,6 +34,7 @@ for n in (1, 2, 4, 8):
         if it:
             times.append(e0.elapsed_time(e1))
     res[n] = sum(times) / len(times)
-out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(res[1] / (n * t), 4)} for n, t in res.items()}
+base = res[ns[0]] * ns[0]
+out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(base / (n * t), 4)} for n, t in res.items()}
 out["env"] = {k: v for k, v in os.environ.items() if k.startswith("NRT_")}
 print(json.dumps(out))
