@@ -2,25 +2,42 @@
 """bench.py — BASELINE.json metric: Msamples/s on cornell-box-scene.json at
 1024x1024, spp=256, over 1/2/4/8 GPUs.
 
-One "step" = one full render of the frame: every rank renders the image rows
-y = rank (mod N) with the HIP megakernel (libnrt.so, inputs already resident in
-HBM), then one RCCL gather (torch.distributed "nccl" backend = RCCL over xGMI)
-brings the rows to rank 0, which un-permutes them into the final framebuffer in
-HBM.  The frame is fixed as N grows, so scaling is "strong".
+One "step" = one full frame, ending with the framebuffer in host memory (the
+reference times `scene.render`, which returns a host `Rgb32FImage`,
+app/commands/render.rs:57-62, camera.rs:342):
+
+  * every rank renders the image rows y = rank (mod N) with the HIP megakernel
+    (libnrt.so; the scene is resident in HBM since upload),
+  * N > 1: one RCCL gather (torch.distributed "nccl" = RCCL over xGMI) of the row
+    buffers to rank 0, which un-permutes them into the frame in HBM,
+  * rank 0 copies the frame to pinned host memory on a copy stream.  Frames are
+    double-buffered, so frame k's device-to-host copy overlaps frame k+1's render
+    (as a render loop would run); the timed region ends when the last frame is
+    on the host.
+
+The frame is fixed as N grows, so scaling is "strong".
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  The roofline block reports the render kernel's
-achieved HBM bandwidth (algorithmic bytes / kernel time, HIP events on the
-launch stream) against the 8 TB/s gfx950 peak; PMC-counted traffic comes from
-the committed rocprofv3 summary when present.  The cpu_baseline leg times the
-oracle (the C++ f64 restatement; the Rust reference cannot be built here) on a
+Rank 0 prints one JSON line.  `roofline` prices the render kernel against the
+bound that limits it, the FP32 (or FP64) VALU peak: achieved = SURVEY §8(d)'s
+algorithmic FLOPs per sample (oracle event counts x per-event costs,
+tests/golden/work_counts.json) x samples per launch / the kernel's HIP-event
+time on its launch stream.  The HBM figures the north star asks for sit beside
+it (`roofline.hbm`): framebuffer + scene bytes per launch over the same time,
+and rocprofv3 FETCH_SIZE/WRITE_SIZE traffic from profiles/pmc_summary.json,
+looked up by (scene, size, spp, precision, rng, trace).  The cpu_baseline leg
+times the oracle (the C++ f64 restatement; the Rust reference cannot be built
+here), compiled for the host CPU, on every core this process may use, over a
 bounded row sample of the same frame.
 """
 import argparse
+import hashlib
 import json
+import math
 import os
+import platform
 import subprocess
 import sys
 import tempfile
@@ -32,7 +49,7 @@ sys.path.insert(0, os.path.join(ROOT, "nr-ray-tracer_amd"))
 METRIC = "Msamples/sec on Cornell box 1024x1024 spp=256; 1/2/4/8-GPU scaling"
 DEFAULT_SCENE = "scenes/cornell-box-scene.json"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}
+VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}  # 256 CUs x 2.4 GHz (vendor figures)
 
 # device record sizes (device_scene.hpp) for the algorithmic byte count
 REC = {"f32": dict(node=32, prim=80, xform=112), "f64": dict(node=64, prim=144, xform=208)}
@@ -44,15 +61,60 @@ def scene_bytes(stats, precision):
             + stats["instances"] * 16 + stats["materials"] * 16 + stats["textures"] * 64 + stats["texels"] * 12)
 
 
-def cpu_baseline(args, samples_note):
+# ------------------------------------------------------------------ CPU baseline
+
+def host_cpus():
+    """(cores this process may run on, description): the affinity set, capped by a cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as fh:
+                q, p = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(p)
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    desc = f"{model}; os.cpu_count()={os.cpu_count()}, affinity={aff}, cgroup quota={quota if quota else 'none'}"
+    return cores, model, desc
+
+
+def native_oracle():
+    """The oracle compiled for this host's CPU (-march=native; same IEEE arithmetic, -ffp-contract=off),
+    cached per CPU model; the portable in-tree build if no compiler is available."""
+    _, model, _ = host_cpus()
+    tag = hashlib.sha256(model.encode()).hexdigest()[:12]
+    path = os.path.join(ROOT, "oracle", "build", f"oracle_native_{tag}")
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        r = subprocess.run(["g++", "-std=c++17", "-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math",
+                            "-pthread", "-o", path, os.path.join(ROOT, "oracle", "oracle.cpp")],
+                           capture_output=True)
+        if r.returncode != 0:
+            path = os.path.join(ROOT, "oracle", "build", "oracle")
+            if not os.path.exists(path):
+                subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+            return path, "portable -O3 build (g++ -march=native failed)"
+    return path, "g++ -O3 -march=native -ffp-contract=off"
+
+
+def cpu_baseline(args):
     """Oracle (test infrastructure) timed on the host cores over a row sample."""
     sys.path.insert(0, ROOT)
     from oracle import scene_tree
 
-    oracle_bin = os.path.join(ROOT, "oracle", "build", "oracle")
-    if not os.path.exists(oracle_bin):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    threads = min(16, os.cpu_count() or 1)
+    oracle_bin, build = native_oracle()
+    threads, _, desc = host_cpus()
     with tempfile.TemporaryDirectory() as td:
         old = os.getcwd()
         os.chdir(os.path.join(ROOT, "tests", "golden"))
@@ -75,23 +137,32 @@ def cpu_baseline(args, samples_note):
     return {"value": round(info["msamples_per_s"], 4), "unit": "Msamples/s", "cores": info["threads"],
             "kind": "port",
             "sample": f"rows y%{stride}==0 of {args.width}x{args.height} at spp={args.spp} ({rows} rows, "
-                      f"{info['samples'] / 1e6:.1f} Msamples, {info['seconds']:.1f} s); oracle = C++ f64 "
-                      f"restatement, per-pixel dynamic scheduling; Rust reference unbuildable (no toolchain)"}
+                      f"{info['samples'] / 1e6:.1f} Msamples, {info['seconds']:.2f} s wall, "
+                      f"{info['seconds'] * info['threads']:.1f} CPU-s); oracle = C++ f64 restatement of the "
+                      f"reference path ({build}), per-pixel dynamic scheduling over all usable cores; "
+                      f"Rust reference unbuildable (no toolchain)",
+            "cpu": desc}
 
 
-def load_pmc(precision, rng):
-    """The committed rocprofv3 PMC summary of this kernel variant (profiles/pmc_summary.json), or {}."""
+# ------------------------------------------------------------------ committed evidence lookups
+
+def load_pmc(key):
+    """The committed rocprofv3 summary of exactly this kernel variant and config, or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return {}
     try:
         with open(path) as fh:
-            return json.load(fh).get(f"{precision}_{rng}", {}) or {}
+            entries = json.load(fh).get("entries", [])
     except Exception:
         return {}
+    for e in entries:
+        if all(e.get(k) == v for k, v in key.items()):
+            return e
+    return {}
 
 
-def load_work(scene, w, h):
+def load_work(scene, w, h, spp):
     """Per-sample algorithmic work of this config (tests/golden/work_counts.json), or None."""
     path = os.path.join(ROOT, "tests", "golden", "work_counts.json")
     if not os.path.exists(path):
@@ -104,17 +175,7 @@ def load_work(scene, w, h):
     return None
 
 
-def work_block(wc, msamples_per_s, precision):
-    """rays/s and the algorithmic VALU-FLOP fraction (oracle event counts x SURVEY §8(d) costs)."""
-    if wc is None:
-        return None
-    tflops = wc["flops_per_sample"] * msamples_per_s * 1e6 / 1e12
-    return {"rays_per_s": round(wc["rays_per_sample"] * msamples_per_s * 1e6, 1),
-            "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"],
-            "algorithmic_tflops": round(tflops, 3), "valu_peak_tflops": VALU_PEAK_TFLOPS[precision],
-            "valu_flop_frac": round(tflops / VALU_PEAK_TFLOPS[precision], 4),
-            "source": f"tests/golden/work_counts.json[{wc['name']}] (oracle event counts, ChaCha8 stream)"}
-
+# ------------------------------------------------------------------ main
 
 def main():
     ap = argparse.ArgumentParser()
@@ -136,13 +197,13 @@ def main():
     import torch
     import torch.distributed as dist
     import nrt
+    from nrt import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    if world != args.gpus and world == 1:
+        raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
@@ -163,53 +224,92 @@ def main():
     scene.upload(local)
     t_upload = time.perf_counter() - t0
 
-    from nrt import shard
-
     rows_max = shard.rows_max(H, world)
     rows = scene.rows_selected(H, rank, world)
     assert rows == shard.rows_of(H, rank, world)
     buf = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev)
-    final = torch.empty((H, W, 3), dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
     stream = torch.cuda.current_stream()
-    ev = []
+    lead = rank == 0
+    # double-buffered frames: render targets (N = 1) or gathered frames (N > 1, rank 0) in HBM,
+    # and pinned host frames
+    rbuf = [buf, torch.zeros_like(buf)] if world == 1 else [buf]
+    if lead:
+        frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
+                                          for _ in range(2)]
+        host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(2)]
+        copy_stream = torch.cuda.Stream(device=dev)
+        copied = [None, None]
+    kev, cev = [], []
 
-    def step(timed):
+    def step(k, timed):
+        slot = k % 2
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        target = rbuf[slot % len(rbuf)]
+        if world == 1 and copied[slot] is not None:
+            stream.wait_event(copied[slot])  # render target `slot` was copied out two frames ago
         e0.record(stream)
-        scene.render_device(buf.data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng, device=local,
+        scene.render_device(target.data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng, device=local,
                             row_offset=rank, row_stride=world, stream=stream.cuda_stream, trace=args.trace)
         e1.record(stream)
         if timed:
-            ev.append((e0, e1))
+            kev.append((e0, e1))
         if world > 1:  # the single RCCL collective + un-permute on rank 0
-            shard.gather_frame(buf, H, dist, rank, world, out=final)
+            fr = frames[slot] if lead else None
+            if lead and copied[slot] is not None:
+                stream.wait_event(copied[slot])  # frame buffer `slot` was copied out two frames ago
+            shard.gather_frame(buf, H, dist, rank, world, out=fr)
+        if lead:
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            copy_stream.wait_event(ready)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            src = frames[slot]
+            with torch.cuda.stream(copy_stream):
+                c0.record(copy_stream)
+                host[slot].view(-1).copy_(src.view(-1)[: H * W * 3], non_blocking=True)
+                c1.record(copy_stream)
+            copied[slot] = c1
+            if timed:
+                cev.append((c0, c1))
 
-    for _ in range(args.warmup):
-        step(False)
+    for k in range(args.warmup):
+        step(k, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
+    for k in range(args.steps):
+        step(args.warmup + k, True)
+    torch.cuda.synchronize()  # every frame's device-to-host copy has landed
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    kern_ms = sum(a.elapsed_time(b) for a, b in kev) / max(len(kev), 1)
+    d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
-    if rank == 0:
+    if lead:
+        last = host[(args.warmup + args.steps - 1) % 2].numpy()
+        frame_sha = hashlib.sha256(last.tobytes()).hexdigest()
         samples = float(W) * H * spp
         value = samples * args.steps / elapsed / 1e6
         st = scene.stats()
         alg_bytes = rows * W * 12 + scene_bytes(st, args.precision)
-        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        pmc = load_pmc(args.precision, args.rng) if args.scene == DEFAULT_SCENE else {}
+        hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        key = {"scene": args.scene, "width": W, "height": H, "spp": spp, "precision": args.precision,
+               "rng": args.rng, "trace": args.trace, "n_gpus": world}
+        pmc = load_pmc(key)
         traffic = pmc.get("hbm_bytes_per_launch")
+        wc = load_work(args.scene, W, H, spp)
+        peak = VALU_PEAK_TFLOPS[args.precision]
+        if wc is not None:
+            flops_launch = wc["flops_per_sample"] * rows * W * spp  # this rank's launch
+            achieved = flops_launch / (kern_ms / 1e3) / 1e12
+        else:
+            flops_launch, achieved = None, None
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -219,20 +319,34 @@ def main():
                        "width": W, "height": H, "spp": spp, "ray_max_bounces": cam.ray_max_bounces,
                        "rng": args.rng, "precision": args.precision, "trace": args.trace,
                        "world_prims": st["world_prims"],
-                       "parallelism": f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 3), "algorithmic_bytes_per_launch": alg_bytes,
-                         "note": "path is VALU-issue-bound (no dense contraction, no MFMA); HBM fraction is "
-                                 "reported as the north star asks",
-                         "valu_issue_frac": pmc.get("valu_issue_frac"),
-                         "valu_lane_utilization": pmc.get("valu_lane_utilization"),
-                         "pmc_source": "profiles/pmc_summary.json" if pmc else None},
-            "work": work_block(load_work(args.scene, W, H), value, args.precision),
+                       "parallelism": f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
+                       "timed_step": "render + (N>1) gather/un-permute + device-to-host copy of the frame "
+                                     "(pinned, double-buffered: frame k's copy overlaps frame k+1's render)"},
+            "roofline": {
+                "bound": "valu", "achieved": None if achieved is None else round(achieved, 3), "peak": peak,
+                "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / peak, 4),
+                "traffic": traffic,
+                "flops_per_launch": flops_launch, "kernel_ms": round(kern_ms, 3),
+                "flops_source": None if wc is None else
+                f"tests/golden/work_counts.json[{wc['name']}]: {wc['flops_per_sample']} algorithmic FLOPs/sample "
+                f"(oracle event counts x SURVEY §8(d) per-event costs) x {rows * W * spp} samples per launch",
+                "hbm": {"achieved": round(hbm_achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
+                        "traffic": traffic},
+                "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
+                                                "wait_inst_frac", "source")} if pmc else None,
+                "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
+                        "divergence; its HBM traffic is the framebuffer plus a few KB of scene"},
+            "work": None if wc is None else {
+                "rays_per_s": round(wc["rays_per_sample"] * value * 1e6, 1),
+                "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"]},
+            "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
+                           "frame_wall": round(elapsed / args.steps * 1e3, 3)},
             "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4)},
+            "frame_sha256": frame_sha,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, None)
+            out["cpu_baseline"] = cpu_baseline(args)
         elif not args.no_cpu_baseline:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
