@@ -162,8 +162,9 @@ def load_pmc(key):
     return {}
 
 
-def load_work(scene, w, h, spp):
-    """Per-sample algorithmic work of this config (tests/golden/work_counts.json), or None."""
+def load_work(scene, w, h, spp=None):
+    """Per-sample algorithmic work of this config (tests/golden/work_counts.json), or None.
+    Per-sample counts do not depend on spp (samples of a pixel are independent)."""
     path = os.path.join(ROOT, "tests", "golden", "work_counts.json")
     if not os.path.exists(path):
         return None
@@ -173,6 +174,19 @@ def load_work(scene, w, h, spp):
         if c["scene"] == scene and c["width"] == w and c["height"] == h:
             return dict(c, name=name)
     return None
+
+
+def work_block(wc, msamples_per_s, precision):
+    """rays/s and the algorithmic VALU-FLOP rate of a whole-job throughput (oracle event counts x
+    SURVEY §8(d) per-event costs)."""
+    if wc is None:
+        return None
+    tflops = wc["flops_per_sample"] * msamples_per_s * 1e6 / 1e12
+    return {"rays_per_s": round(wc["rays_per_sample"] * msamples_per_s * 1e6, 1),
+            "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"],
+            "algorithmic_tflops": round(tflops, 3), "valu_peak_tflops": VALU_PEAK_TFLOPS[precision],
+            "valu_flop_frac": round(tflops / VALU_PEAK_TFLOPS[precision], 4),
+            "source": f"tests/golden/work_counts.json[{wc['name']}] (oracle event counts, ChaCha8 stream)"}
 
 
 # ------------------------------------------------------------------ main
@@ -337,9 +351,7 @@ def main():
                                                 "wait_inst_frac", "source")} if pmc else None,
                 "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
                         "divergence; its HBM traffic is the framebuffer plus a few KB of scene"},
-            "work": None if wc is None else {
-                "rays_per_s": round(wc["rays_per_sample"] * value * 1e6, 1),
-                "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"]},
+            "work": work_block(wc, value, args.precision),
             "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
                            "frame_wall": round(elapsed / args.steps * 1e3, 3)},
             "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4)},

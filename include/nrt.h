@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 1
+#define NRT_ABI_VERSION 2
 
 enum {
     NRT_OK = 0,
@@ -127,6 +127,9 @@ typedef struct {
     uint64_t device_bytes; /* HBM bytes of the flattened scene on one device */
     uint64_t world_prims;  /* world-list test units after flattening instances to world space: primitives,
                               with six quads closing a box counted once (0: not flattenable) */
+    uint32_t coplanar_pairs; /* overlapping coplanar surface pairs (their hits tie in the reference) */
+    uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
+                                (else AUTO takes the world BVH, which compares tie keys) */
 } nrt_scene_stats;
 
 typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);

@@ -495,6 +495,8 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
                             f.inst_fast.size() * sizeof(DInstFast<float>) + f.mats_fast.size() * sizeof(DMatFast) +
                             f.wprims.size() * sizeof(DPrimWorld<float>);
         out->world_prims = f.world_ok ? f.world_units : 0;
+        out->coplanar_pairs = f.coplanar_pairs;
+        out->world_list_ok = f.world_ok && f.list_ok ? 1u : 0u;
         return NRT_OK;
     });
 }

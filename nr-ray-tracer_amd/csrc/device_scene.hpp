@@ -104,12 +104,22 @@ struct alignas(16) DPrimWorld {
 // plane coordinate folded into a0' = a0 - A_a P, b0' = b0 - B_a P.
 // PRIM_BOX (world mode): six consecutive quads that close a parallelepiped
 // {c + a e1 + b e2 + g e3 : a, b, g in [0, 1]} are tested as one slab test in
-// its local frame x' = E^-1 x - E^-1 c.  The header entry holds the rows of
-// E^-1 and E^-1 c as (N, D), (AB[0..2], AB[3]), (AB[4..6], AB[7]); meta =
-// PRIM_BOX | face << 3 with 3 bits per (axis, side) naming which of the six
-// quads that follow the header lies on plane x'_axis = side.  The quads keep
-// their own records (uv, normals, material) for the hit record.
+// a local frame: per axis k, l_k(x) = row_k . x with faces on l_k = D_k and
+// l_k = D_k + L_k (row_k = s_k (E^-1)_k, D_k = s_k (E^-1 c)_k, L_k = |s_k|; the
+// scale makes a row's largest entry a power of two, flatten.cpp fuse_box).  The
+// header holds (row_0, D_0) in (N, D), (row_1, D_1) in (AB[0..2], AB[3]),
+// (row_2, D_2) in (AB[4..6], AB[7]), L in S; meta = PRIM_BOX | face << 3 with
+// 3 bits per (axis, side) naming which of the six quads that follow the header
+// lies on plane l_axis = D + side * L.  The quads keep their own records (uv,
+// normals, material) for the hit record.
 constexpr uint32_t BOX_ENTRIES = 7;
+// PRIM_BOXY (world-list run kind only; header meta kind stays PRIM_BOX): a box turned
+// about the world y axis only.  Local axes (A, y, B): (N[0], N[2], D) = x, z entries
+// of row A and its offset, (AB[0], AB[2], AB[3]) the same for row B (their y entries
+// are 0), AB[4] <= AB[5] = the world y of the bottom and top faces, whose slab is the
+// world y slab of axis quads and rooms (t = fma(Y, 1/d_y, -o_y/d_y)); face slots as
+// PRIM_BOX with axis 1 = y (side 0 = bottom).
+constexpr uint32_t PRIM_BOXY = 8;
 // PRIM_ABOX (world list): axis quads that each cover a whole face of one axis-
 // aligned box (a "room": the Cornell walls) as one slab test; header N = lo,
 // AB[0..2] = hi, meta = PRIM_ABOX | face slots << 3 (3 bits per (axis, side),
@@ -118,9 +128,27 @@ constexpr uint32_t BOX_ENTRIES = 7;
 // and t >= t_min, otherwise the exit face if present (the box is convex).
 constexpr uint32_t ABOX_PRESENT_SHIFT = 21;
 constexpr uint32_t WFLAG_AXIS_QUADS = 1;
-// Consecutive units of one kind form a run (kind | count << 2; a box unit is
-// BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised
+// Coplanar overlapping surfaces (e.g. a cube standing on the Cornell floor: its
+// bottom face and the floor quad share the plane y = 0).  The reference resolves
+// their hits as an exact tie -- its t is bit-identical on both -- in favour of the
+// later candidate of its depth-first order (BVH::hit, object.rs:109-115).  The host
+// marks the pair's later surface WCLASS_WIN and the earlier WCLASS_LOSE (top bits of
+// meta; box / room headers: the class of their faces).
+//  * World list: units are ordered losers first, winners last, and `t <= t_best` lets
+//    the later of two equal t win; the flattener keeps the list only when each pair's
+//    two f32 t formulas are provably bit-identical (flatten.cpp tie forms), so the
+//    hot loop pays nothing.
+//  * World BVH (any visiting order, any formulas): with WFLAG_COPLANAR the leaf test
+//    compares keys, t * (1 - WTIE_EPS) for winners and t * (1 + WTIE_EPS) for losers,
+//    so near-ties go the reference's way; the hit record divides the factor out.
+constexpr uint32_t WCLASS_SHIFT = 30, WCLASS_WIN = 1, WCLASS_LOSE = 2;
+constexpr uint32_t WMAT_MASK = (1u << (WCLASS_SHIFT - WKIND_BITS)) - 1u;  // material index bits of meta
+constexpr uint32_t WFLAG_COPLANAR = 2;
+constexpr float WTIE_EPS = 1.0f / 1048576.0f;  // 2^-20: 16 ulps of f32
+// Consecutive units of one kind form a run (kind | count << WRUN_KIND_BITS; a box
+// unit is BOX_ENTRIES entries), so the kernel's inner loops are kind-specialised
 // without reordering candidates.
+constexpr uint32_t WRUN_KIND_BITS = 4, WRUN_KIND_MASK = 15;
 
 // Fast kernel, world-BVH mode (large flattenable scenes): a binary BVH over the
 // world-space primitives built with binned SAH on the host.  Each node holds

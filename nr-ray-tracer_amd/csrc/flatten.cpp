@@ -475,6 +475,11 @@ struct Flattener {
             ++nfaces;
         }
         if (nfaces < 2) return;
+        uint32_t cls = 0;  // the faces' coplanar-tie class (device_scene.hpp WCLASS_*), one per unit
+        for (int a = 0; a < 3; ++a)
+            for (int sd = 0; sd < 2; ++sd)
+                if (face[a][sd] >= 0) cls |= units[face[a][sd]][0].meta >> WCLASS_SHIFT;
+        if (cls == (WCLASS_WIN | WCLASS_LOSE)) return;
         std::vector<DPrimWorld<double>> unit(1 + 6);
         DPrimWorld<double>& h = unit[0];
         h = DPrimWorld<double>{};
@@ -485,6 +490,7 @@ struct Flattener {
             for (int sd = 0; sd < 2; ++sd) {
                 const int slot = 2 * a + sd;
                 if (face[a][sd] >= 0) {
+                    if (src[face[a][sd]] != SIZE_MAX) tie_form[src[face[a][sd]]] = axis_form(a, sd ? hi[a] : lo[a]);
                     unit[1 + slot] = units[face[a][sd]][0];
                     map |= (uint32_t)slot << (3 * slot);
                     present |= 1u << slot;
@@ -494,7 +500,7 @@ struct Flattener {
                     map |= 7u << (3 * slot);
                 }
             }
-        h.meta = PRIM_ABOX | (map << WKIND_BITS) | (present << ABOX_PRESENT_SHIFT);
+        h.meta = PRIM_ABOX | (map << WKIND_BITS) | (present << ABOX_PRESENT_SHIFT) | (cls << WCLASS_SHIFT);
         std::vector<std::vector<DPrimWorld<double>>> nu;
         std::vector<uint32_t> nk;
         std::vector<size_t> ns;
@@ -509,7 +515,7 @@ struct Flattener {
     }
 
     // Six consecutive quads closing a parallelepiped -> PRIM_BOX header (device_scene.hpp).
-    bool fuse_box(size_t i, DPrimWorld<double>& hdr) const {
+    bool fuse_box(size_t i, DPrimWorld<double>& hdr) {
         std::vector<V3a> pts;
         double scale = 0;
         for (size_t q = i; q < i + 6; ++q) {
@@ -586,7 +592,44 @@ struct Flattener {
             if (onaxis < 0 || combos != 2 || face[onaxis][side] >= 0) return false;
             face[onaxis][side] = (int)q;
         }
+        uint32_t cls = 0;  // the faces' coplanar-tie class (device_scene.hpp WCLASS_*), one per unit
+        for (size_t q = 0; q < 6; ++q) cls |= out.wprims[i + q].meta >> WCLASS_SHIFT;
+        if (cls == (WCLASS_WIN | WCLASS_LOSE)) return false;
         hdr = DPrimWorld<double>{};
+        // A box turned about the world y axis only (one edge exactly along y, the others with
+        // y = 0: the common "object standing on a floor") -> PRIM_BOXY: its y slab is the
+        // world y slab the axis quads and rooms use (t = fma(Y, 1/d_y, -o_y/d_y)), so a face
+        // on a floor plane ties bit for bit with the floor, and it costs two rows, not three.
+        int ya = -1;
+        const V3a ed[3] = {e1, e2, e3};
+        for (int a = 0; a < 3; ++a)
+            if (ed[a][0] == 0.0 && ed[a][2] == 0.0 && ed[a][1] != 0.0 && ed[(a + 1) % 3][1] == 0.0 &&
+                ed[(a + 2) % 3][1] == 0.0)
+                ya = a;
+        auto row = [&](int a) { return V3a{Ei[0 + a], Ei[3 + a], Ei[6 + a]}; };  // column-major Ei[3*col + row]
+        if (ya >= 0) {
+            const int A = ya == 0 ? 1 : 0, B = ya == 2 ? 1 : 2;
+            double y0 = c[1], y1 = c[1] + ed[ya][1];
+            int f0 = face[ya][0], f1 = face[ya][1];
+            if (y1 < y0) { std::swap(y0, y1); std::swap(f0, f1); }
+            const V3a ra = row(A), rb = row(B);
+            hdr.N[0] = ra[0]; hdr.N[2] = ra[2]; hdr.D = cl[A];
+            hdr.AB[0] = rb[0]; hdr.AB[2] = rb[2]; hdr.AB[3] = cl[B];
+            hdr.AB[4] = y0; hdr.AB[5] = y1;
+            const int slots[3][2] = {{face[A][0], face[A][1]}, {f0, f1}, {face[B][0], face[B][1]}};
+            uint32_t map = 0;
+            for (int a = 0; a < 3; ++a)
+                for (int sd = 0; sd < 2; ++sd) map |= (uint32_t)slots[a][sd] << (3 * (2 * a + sd));
+            hdr.meta = PRIM_BOX | (map << WKIND_BITS) | (cls << WCLASS_SHIFT);
+            tie_form[i + f0] = axis_form(1, y0);
+            tie_form[i + f1] = axis_form(1, y1);
+            for (int a : {A, B})
+                for (int sd = 0; sd < 2; ++sd)
+                    tie_form[i + face[a][sd]] = {5.0f, (float)row(a)[0], (float)row(a)[2], (float)cl[a], (float)sd};
+            box_y = true;
+            return true;
+        }
+        box_y = false;
         for (int k = 0; k < 3; ++k) {  // rows of E^-1 (column-major Ei[3*col + row])
             hdr.N[k] = Ei[3 * k + 0];
             hdr.AB[k] = Ei[3 * k + 1];
@@ -598,10 +641,127 @@ struct Flattener {
         uint32_t map = 0;
         for (int a = 0; a < 3; ++a)
             for (int sd = 0; sd < 2; ++sd) map |= (uint32_t)face[a][sd] << (3 * (2 * a + sd));
-        hdr.meta = PRIM_BOX | (map << WKIND_BITS);
+        hdr.meta = PRIM_BOX | (map << WKIND_BITS) | (cls << WCLASS_SHIFT);
+        for (int a = 0; a < 3; ++a) {  // tie forms of the six faces (local axis a, side sd), in f32
+            const V3a r = row(a);
+            const float rf[3] = {(float)r[0], (float)r[1], (float)r[2]};
+            const float off = (float)cl[a];
+            int nz = -1, count = 0;
+            for (int k = 0; k < 3; ++k)
+                if (rf[k] != 0.0f) { nz = k; ++count; }
+            int e = 0;
+            const bool pow2 = count == 1 && std::fabs(std::frexp(rf[nz], &e)) == 0.5f;
+            for (int sd = 0; sd < 2; ++sd) {
+                if (sd == 0 && off == 0.0f && pow2) tie_form[i + face[a][sd]] = {1.0f, (float)nz};
+                else tie_form[i + face[a][sd]] = {3.0f, rf[0], rf[1], rf[2], off, (float)sd};
+            }
+        }
         return true;
     }
     static double vdot(const V3a& a, const V3a& c) { return a[0] * c[0] + a[1] * c[1] + a[2] * c[2]; }
+
+    // Coplanar overlapping planar primitives (device_scene.hpp WCLASS_*): the later one
+    // of each pair in the reference's depth-first candidate order (= wprims order, which
+    // world_walk emits left before right) wins the reference's exact tie; mark it
+    // WCLASS_WIN and the earlier WCLASS_LOSE.  A primitive that would be both leaves the
+    // world modes off (the instance BVH keeps the reference's order exactly).
+    // f32 t formula of each world-list face (wprims index before fusion).  Two faces with
+    // equal forms compute bit-identical t in the kernel's world list:
+    //   {1, a}           t = -(o_a * 1/d_a): an axis plane at 0 -- axis quads and room faces
+    //                    (fma(0, 1/d, -o/d)) and box faces on local plane 0 whose E^-1 row is
+    //                    one power of two c on world axis a with offset 0 (c cancels exactly);
+    //   {2, a, P}        t = fma(P, 1/d_a, -o_a/d_a): axis quads and room faces;
+    //   {3, row, off, s} a box face (local slab formula);
+    //   {4, N, D}        t = (D - N.o) / (N.d): quads and triangles.
+    std::map<size_t, std::vector<float>> tie_form;
+    bool box_y = false;  // the last fused box is a PRIM_BOXY unit
+    std::vector<std::pair<size_t, size_t>> tie_pairs;  // (loser, winner) wprims indices
+    static std::vector<float> axis_form(int a, double P) {
+        const float p32 = (float)P;
+        return p32 == 0.0f ? std::vector<float>{1.0f, (float)a} : std::vector<float>{2.0f, (float)a, p32};
+    }
+
+    bool mark_coplanar() {
+        struct Pl { size_t i; V3a n; double d; };
+        std::vector<Pl> pl;
+        double scale = 0;
+        for (size_t i = 0; i < out.wprims.size(); ++i) {
+            const uint32_t kind = out.wprims[i].meta & WKIND_MASK;
+            if (kind != PRIM_QUAD && kind != PRIM_TRIANGLE) continue;
+            const auto& g = wgeom[i];
+            V3a n = {g[1][1] * g[2][2] - g[1][2] * g[2][1], g[1][2] * g[2][0] - g[1][0] * g[2][2],
+                     g[1][0] * g[2][1] - g[1][1] * g[2][0]};
+            const double len = std::sqrt(vdot(n, n));
+            if (!(len > 0) || !std::isfinite(len)) continue;
+            for (double& c : n) c /= len;
+            for (int k = 0; k < 3; ++k)  // canonical orientation: first clearly non-zero component positive
+                if (std::fabs(n[k]) > 1e-12) {
+                    if (n[k] < 0) for (double& c : n) c = -c;
+                    break;
+                }
+            for (int k = 0; k < 3; ++k) scale = std::max({scale, std::fabs(g[0][k]), std::fabs(g[0][k] + g[1][k] + g[2][k])});
+            pl.push_back({i, n, vdot(n, g[0])});
+        }
+        const double tol = 1e-9 * std::max(scale, 1e-300);
+        std::sort(pl.begin(), pl.end(), [](const Pl& a, const Pl& b) { return a.d < b.d; });
+        auto corners = [&](size_t i, std::vector<V3a>& c) {
+            const auto& g = wgeom[i];
+            const bool quad = (out.wprims[i].meta & WKIND_MASK) == PRIM_QUAD;
+            c = {g[0], {g[0][0] + g[1][0], g[0][1] + g[1][1], g[0][2] + g[1][2]}};
+            if (quad) c.push_back({g[0][0] + g[1][0] + g[2][0], g[0][1] + g[1][1] + g[2][1], g[0][2] + g[1][2] + g[2][2]});
+            c.push_back({g[0][0] + g[2][0], g[0][1] + g[2][1], g[0][2] + g[2][2]});
+        };
+        // positive-area overlap of two convex polygons in one plane (separating axis test;
+        // polygons that only touch along an edge or at a corner do not overlap)
+        auto overlap = [&](const Pl& a, size_t j) {
+            std::vector<V3a> pa, pb;
+            corners(a.i, pa);
+            corners(j, pb);
+            V3a e1 = {pa[1][0] - pa[0][0], pa[1][1] - pa[0][1], pa[1][2] - pa[0][2]};
+            const double l1 = std::sqrt(vdot(e1, e1));
+            for (double& c : e1) c /= l1;
+            const V3a e2 = {a.n[1] * e1[2] - a.n[2] * e1[1], a.n[2] * e1[0] - a.n[0] * e1[2], a.n[0] * e1[1] - a.n[1] * e1[0]};
+            auto flat = [&](const std::vector<V3a>& p) {
+                std::vector<std::array<double, 2>> q;
+                for (const V3a& x : p) q.push_back({vdot(x, e1), vdot(x, e2)});
+                return q;
+            };
+            const auto qa = flat(pa), qb = flat(pb);
+            for (const auto* poly : {&qa, &qb})
+                for (size_t k = 0; k < poly->size(); ++k) {
+                    const auto& u = (*poly)[k];
+                    const auto& v = (*poly)[(k + 1) % poly->size()];
+                    const double ax = -(v[1] - u[1]), ay = v[0] - u[0];
+                    double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+                    for (const auto& x : qa) { const double t = ax * x[0] + ay * x[1]; amin = std::min(amin, t); amax = std::max(amax, t); }
+                    for (const auto& x : qb) { const double t = ax * x[0] + ay * x[1]; bmin = std::min(bmin, t); bmax = std::max(bmax, t); }
+                    const double slack = tol * std::sqrt(ax * ax + ay * ay);
+                    if (amax <= bmin + slack || bmax <= amin + slack) return false;
+                }
+            return true;
+        };
+        std::vector<uint32_t> cls(out.wprims.size(), 0);
+        bool any = false;
+        for (size_t a = 0; a < pl.size(); ++a)
+            for (size_t b = a + 1; b < pl.size() && pl[b].d - pl[a].d <= tol; ++b) {
+                const V3a& na = pl[a].n;
+                const V3a& nb = pl[b].n;
+                if (std::fabs(na[0] - nb[0]) > 1e-9 || std::fabs(na[1] - nb[1]) > 1e-9 || std::fabs(na[2] - nb[2]) > 1e-9) continue;
+                if (!overlap(pl[a], pl[b].i)) continue;
+                const size_t lo = std::min(pl[a].i, pl[b].i), hi = std::max(pl[a].i, pl[b].i);
+                cls[lo] |= WCLASS_LOSE;
+                cls[hi] |= WCLASS_WIN;
+                tie_pairs.emplace_back(lo, hi);
+                any = true;
+            }
+        for (size_t i = 0; i < cls.size(); ++i) {
+            if (cls[i] == (WCLASS_WIN | WCLASS_LOSE)) return false;
+            out.wprims[i].meta |= cls[i] << WCLASS_SHIFT;
+        }
+        if (any) out.wflags |= WFLAG_COPLANAR;
+        out.coplanar_pairs = (uint32_t)tie_pairs.size();
+        return true;
+    }
 
     void world_walk(const Object* o, const Affine& f) {
         if (!out.world_ok) return;
@@ -615,7 +775,9 @@ struct Flattener {
                 const V3a c = va(o->center);
                 for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.AB[k] = va(o->speed)[k]; }
                 w.D = o->radius;
-                w.meta = PRIM_SPHERE | (material(o->material) << WKIND_BITS);
+                const uint32_t mat = material(o->material);
+                if (mat > WMAT_MASK) { out.world_ok = false; return; }
+                w.meta = PRIM_SPHERE | (mat << WKIND_BITS);
                 out.wprims.push_back(w);
                 wgeom.push_back({});
                 break;
@@ -636,7 +798,9 @@ struct Flattener {
                 w.D = o->d - vdot(n, f.b);
                 w.AB[6] = a0 - vdot(Aq, f.b);
                 w.AB[7] = b0 - vdot(Bq, f.b);
-                w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (material(o->material) << WKIND_BITS);
+                const uint32_t mat = material(o->material);
+                if (mat > WMAT_MASK) { out.world_ok = false; return; }
+                w.meta = (o->kind == Object::Quad ? PRIM_QUAD : PRIM_TRIANGLE) | (mat << WKIND_BITS);
                 out.wprims.push_back(w);
                 break;
             }
@@ -784,6 +948,7 @@ struct Flattener {
         out.num_trees = (uint32_t)tree_ranges.size();
         out.world_ok = true;
         world_walk(top, Affine{});
+        if (out.world_ok) out.world_ok = mark_coplanar();
         if (!out.world_ok) out.wprims.clear();
         if (out.world_ok && !out.wprims.empty()) build_wbvh();
         // fuse closed boxes, then group units by kind: one run per kind.  The f32
@@ -798,12 +963,19 @@ struct Flattener {
                 std::vector<DPrimWorld<double>> u{hdr};
                 u.insert(u.end(), out.wprims.begin() + i, out.wprims.begin() + i + 6);
                 units.push_back(std::move(u));
-                unit_kind.push_back(PRIM_BOX);
+                unit_kind.push_back(box_y ? PRIM_BOXY : PRIM_BOX);
                 unit_src.push_back(SIZE_MAX);
                 i += 6;
             } else {
                 DPrimWorld<double> w = out.wprims[i];
                 if ((w.meta & WKIND_MASK) == PRIM_QUAD) axis_quad(w);
+                const uint32_t wk = w.meta & WKIND_MASK;
+                if (wk >= PRIM_QUAD_X && wk <= PRIM_QUAD_Z) {
+                    const int a = (int)(wk - PRIM_QUAD_X);
+                    tie_form[i] = axis_form(a, w.N[(a + 1) % 3]);
+                } else if (wk == PRIM_QUAD || wk == PRIM_TRIANGLE) {
+                    tie_form[i] = {4.0f, (float)w.N[0], (float)w.N[1], (float)w.N[2], (float)w.D};
+                }
                 units.push_back({w});
                 unit_kind.push_back(w.meta & WKIND_MASK);
                 unit_src.push_back(i);
@@ -811,11 +983,34 @@ struct Flattener {
             }
         }
         fuse_room(units, unit_kind, unit_src);
-        static const int rank[8] = {5, 3, 4, 6, 0, 1, 2, 7};  // X, Y, Z quads, quads, triangles, spheres, boxes, rooms
+        // the world list resolves a coplanar tie by order alone: only when both faces compute
+        // bit-identical t (equal tie forms); otherwise the scene uses the world BVH's keys
+        for (const auto& [lo, hi] : tie_pairs) {
+            auto a = tie_form.find(lo), b = tie_form.find(hi);
+            if (a == tie_form.end() || b == tie_form.end() || a->second != b->second) out.list_ok = false;
+            if (std::getenv("NRT_DEBUG_TIES")) {
+                auto pr = [&](size_t i, decltype(a) it) {
+                    fprintf(stderr, "  prim %zu:", i);
+                    if (it != tie_form.end()) for (float v : it->second) fprintf(stderr, " %.9g", v);
+                    fprintf(stderr, "\n");
+                };
+                fprintf(stderr, "tie pair\n");
+                pr(lo, a);
+                pr(hi, b);
+            }
+        }
+        // Order: coplanar-tie losers, then the rest, then winners, by kind within each: the
+        // later of two equal t wins in the kernel (device_scene.hpp WCLASS_*).
+        // X, Y, Z quads, quads, triangles, spheres, y boxes, boxes, rooms
+        static const int rank[9] = {5, 3, 4, 7, 0, 1, 2, 8, 6};
+        auto cls_of = [&](size_t u) { return units[u][0].meta >> WCLASS_SHIFT; };
+        auto phase = [&](size_t u) { return cls_of(u) == WCLASS_LOSE ? 0 : (cls_of(u) == WCLASS_WIN ? 2 : 1); };
         std::vector<size_t> order(units.size());
         for (size_t k = 0; k < order.size(); ++k) order[k] = k;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](size_t a, size_t b) { return rank[unit_kind[a]] < rank[unit_kind[b]]; });
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+            if (phase(a) != phase(b)) return phase(a) < phase(b);
+            return rank[unit_kind[a]] < rank[unit_kind[b]];
+        });
         std::vector<DPrimWorld<double>> fused;
         std::vector<uint32_t> kinds;
         for (size_t k : order) {
@@ -824,10 +1019,11 @@ struct Flattener {
         }
         out.wprims.swap(fused);
         out.world_units = kinds.size();
-        const uint32_t one = 1u << WKIND_BITS;
+        const uint32_t one = 1u << WRUN_KIND_BITS;
         for (uint32_t kind : kinds) {
-            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;  // axis quads and rooms use 1/d
-            if (!out.wruns.empty() && (out.wruns.back() & WKIND_MASK) == kind && (out.wruns.back() >> WKIND_BITS) < (1u << 28))
+            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;  // axis quads, rooms and y boxes use 1/d
+            if (!out.wruns.empty() && (out.wruns.back() & WRUN_KIND_MASK) == kind &&
+                (out.wruns.back() >> WRUN_KIND_BITS) < (1u << 27))
                 out.wruns.back() += one;
             else
                 out.wruns.push_back(kind | one);

@@ -33,6 +33,8 @@ struct FlatScene {
     uint64_t world_units = 0;     // primitives + fused boxes: the world list's test count
     uint32_t wflags = 0;          // WFLAG_* of the world list
     bool world_ok = false;
+    bool list_ok = true;          // the world list reproduces every coplanar tie (flatten.cpp tie forms)
+    uint32_t coplanar_pairs = 0;  // overlapping coplanar primitive pairs (device_scene.hpp WCLASS_*)
     // World BVH over the (unfused) world primitives, for large flattenable scenes.
     WorldBvh wbvh;
     std::vector<DPrimWorld<double>> wbvh_prims;  // BVH leaf order

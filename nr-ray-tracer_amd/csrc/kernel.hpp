@@ -568,6 +568,16 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Axis-aligned quad run (PRIM_QUAD_X + A; device_scene.hpp): t from the per-ray
 // reciprocal, (alpha, beta) from the two in-plane coordinates only.
+// Coplanar-tie key (device_scene.hpp WCLASS_*): t scaled by the unit's tie factor when TIE.
+template <bool TIE>
+__device__ __forceinline__ float tie_key(float t, float f) {
+    if constexpr (TIE) return t * f;
+    else return t;
+}
+__device__ __forceinline__ float tie_factor(uint32_t cls) {
+    return cls == WCLASS_WIN ? 1.0f - WTIE_EPS : (cls == WCLASS_LOSE ? 1.0f + WTIE_EPS : 1.0f);
+}
+
 template <int A>
 __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t& k, uint32_t end, const Ray<float>& ray,
                                               const float inv[3], const float oinv[3], float& t_best, int32_t& best) {
@@ -576,13 +586,142 @@ __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t
     const float* d = &ray.d.x;
     for (; k < end; ++k) {
         const ConstPrimWorld<float> q = wp + k;
-        const float t = q->N[A1] * inv[A] - oinv[A];  // (P - o_a) / d_a
+        const float t = __builtin_fmaf(q->N[A1], inv[A], -oinv[A]);  // (P - o_a) / d_a
         const float p1 = o[A1] + t * d[A1], p2 = o[A2] + t * d[A2];
         const f32x2 ab = f32x2{q->AB[2 * A1], q->AB[2 * A1 + 1]} * p1 + f32x2{q->AB[2 * A2], q->AB[2 * A2 + 1]} * p2 -
                          f32x2{q->AB[6], q->AB[7]};
         const float lo = fminf(ab.x, ab.y);
         const bool ok = (fabsf(d[A]) >= q->N[A2]) & (t >= 0.001f) & (t <= t_best) & (lo >= 0.0f) & (ab.x <= 1.0f) &
                         (ab.y <= 1.0f);
+        t_best = ok ? t : t_best;
+        best = ok ? (int32_t)k : best;
+    }
+}
+
+// The units of one run (kind = the run's kind): closest hit so far in (t_best, best).
+// `t <= t_best`: the later candidate wins an exact tie (the flattener orders the units
+// so that this is the reference's winner of every coplanar tie, device_scene.hpp WCLASS_*).
+template <bool FLAT>
+__device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kind, uint32_t& k, uint32_t count,
+                                          const Ray<float>& ray, const f32x2& dox, const f32x2& doy, const f32x2& doz,
+                                          const float inv[3], const float oinv[3], const uint32_t entry_slot[3],
+                                          float& t_best, int32_t& best) {
+    const uint32_t end = k + count;
+    if (kind == PRIM_QUAD_X) { axis_quad_run<0>(wp, k, end, ray, inv, oinv, t_best, best); return; }
+    if (kind == PRIM_QUAD_Y) { axis_quad_run<1>(wp, k, end, ray, inv, oinv, t_best, best); return; }
+    if (kind == PRIM_QUAD_Z) { axis_quad_run<2>(wp, k, end, ray, inv, oinv, t_best, best); return; }
+    if (kind == PRIM_ABOX) {  // room: axis-aligned box whose present faces are quads
+        for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
+            const ConstPrimWorld<float> q = wp + k;
+            const uint32_t present = q->meta >> ABOX_PRESENT_SHIFT;
+            const float lx = __builtin_fmaf(q->N[0], inv[0], -oinv[0]), hx = __builtin_fmaf(q->AB[0], inv[0], -oinv[0]);
+            const float ly = __builtin_fmaf(q->N[1], inv[1], -oinv[1]), hy = __builtin_fmaf(q->AB[1], inv[1], -oinv[1]);
+            const float lz = __builtin_fmaf(q->N[2], inv[2], -oinv[2]), hz = __builtin_fmaf(q->AB[2], inv[2], -oinv[2]);
+            const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
+            const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
+            const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+            // face slots 2*axis + side (branch-free selects): entry slots from the ray's
+            // direction signs, exit = the opposite side of the exit axis
+            uint32_t e = entry_slot[2], x = entry_slot[2] ^ 1u;
+            e = tn == ny ? entry_slot[1] : e;
+            e = tn == nx ? entry_slot[0] : e;
+            x = tf == fy ? entry_slot[1] ^ 1u : x;
+            x = tf == fx ? entry_slot[0] ^ 1u : x;
+            const bool use_entry = (tn >= 0.001f) & (__builtin_amdgcn_ubfe(present, e, 1) != 0u);
+            const float t = use_entry ? tn : tf;
+            const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) &
+                            (use_entry | (__builtin_amdgcn_ubfe(present, x, 1) != 0u));
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)(k + 1 + (use_entry ? e : x)) : best;  // the face quad's record
+        }
+        return;
+    }
+    if (kind == PRIM_BOXY) {  // box turned about y: two local rows + the world y slab
+        for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
+            const ConstPrimWorld<float> q = wp + k;
+            const f32x2 la = dox * q->N[0] + doz * q->N[2];  // (row_A . d, row_A . o)
+            const f32x2 lb = dox * q->AB[0] + doz * q->AB[2];
+            const float ia = __builtin_amdgcn_rcpf(la.x), ib = __builtin_amdgcn_rcpf(lb.x);
+            const float ax = (q->D - la.y) * ia, az = (q->AB[3] - lb.y) * ib;
+            const float bx = ax + ia, bz = az + ib;
+            const float ay = __builtin_fmaf(q->AB[4], inv[1], -oinv[1]), by = __builtin_fmaf(q->AB[5], inv[1], -oinv[1]);
+            const float nx = fminf(ax, bx), ny = fminf(ay, by), nz = fminf(az, bz);
+            const float fx = fmaxf(ax, bx), fy = fmaxf(ay, by), fz = fmaxf(az, bz);
+            const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+            const bool entry = tn >= 0.001f;
+            const float t = entry ? tn : tf;
+            const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+            const uint32_t sx = ia < 0.0f ? 1u : 0u, sz = ib < 0.0f ? 5u : 4u;
+            uint32_t se = sz, sxit = sz ^ 1u;
+            se = tn == ny ? entry_slot[1] : se;
+            se = tn == nx ? sx : se;
+            sxit = tf == fy ? entry_slot[1] ^ 1u : sxit;
+            sxit = tf == fx ? sx ^ 1u : sxit;
+            const uint32_t slot = entry ? se : sxit;
+            const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
+        }
+        return;
+    }
+    if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
+        for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
+            const ConstPrimWorld<float> q = wp + k;
+            // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
+            const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
+            const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
+            const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
+            const float ix = __builtin_amdgcn_rcpf(lx.x), iy = __builtin_amdgcn_rcpf(ly.x),
+                        iz = __builtin_amdgcn_rcpf(lz.x);
+            const float ax = (q->D - lx.y) * ix, ay = (q->AB[3] - ly.y) * iy, az = (q->AB[7] - lz.y) * iz;
+            // planes l = D and l = D + L per local axis (L_a in S[a]; flatten.cpp fuse_box)
+            const float bx = ax + ix, by = ay + iy, bz = az + iz;  // planes x' = 0 and x' = 1
+            const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+            const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+            // entry face unless it lies before t_min (origin on or inside the box): then the exit face
+            const bool entry = tn >= 0.001f;
+            const float t = entry ? tn : tf;
+            const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+            // face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0),
+            // then the quad that lies there (3 bits per slot in meta)
+            const uint32_t sx = ix < 0.0f ? 1u : 0u, sy = iy < 0.0f ? 3u : 2u, sz = iz < 0.0f ? 5u : 4u;
+            uint32_t se = sz, sxit = sz ^ 1u;
+            se = tn == fminf(ay, by) ? sy : se;
+            se = tn == fminf(ax, bx) ? sx : se;
+            sxit = tf == fmaxf(ay, by) ? sy ^ 1u : sxit;
+            sxit = tf == fmaxf(ax, bx) ? sx ^ 1u : sxit;
+            const uint32_t slot = entry ? se : sxit;
+            const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
+        }
+        return;
+    }
+    if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres (not compiled in)
+        for (; k < end; ++k) {
+            DPrim<float> sp;
+            for (int c = 0; c < 3; ++c) { sp.a[c] = wp[k].N[c]; sp.b[c] = wp[k].AB[c]; }
+            sp.s = wp[k].D;
+            const float t = sphere_t(sp, ray);
+            const bool ok = (t >= 0.0f) & (t <= t_best);
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)k : best;
+        }
+        return;
+    }
+    const bool quad = kind == PRIM_QUAD;
+    for (; k < end; ++k) {
+        const ConstPrimWorld<float> q = wp + k;
+        const f32x2 dn = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];  // (N.d, N.o)
+        const float t = (q->D - dn.y) * __builtin_amdgcn_rcpf(dn.x);
+        const float px = ray.o.x + t * ray.d.x, py = ray.o.y + t * ray.d.y, pz = ray.o.z + t * ray.d.z;
+        const f32x2 ab = f32x2{q->AB[0], q->AB[1]} * px + f32x2{q->AB[2], q->AB[3]} * py +
+                         f32x2{q->AB[4], q->AB[5]} * pz - f32x2{q->AB[6], q->AB[7]};  // (alpha, beta)
+        const float lo = fminf(ab.x, ab.y);
+        // quad closed [0,1]^2 (plane.rs:121-126), triangle open (plane.rs:128-133); a NaN
+        // coordinate can only come from a rejected denominator or t
+        const bool inside = quad ? (lo >= 0.0f) & (ab.x <= 1.0f) & (ab.y <= 1.0f) : (lo > 0.0f) & (ab.x + ab.y < 1.0f);
+        const bool ok = (fabsf(dn.x) >= 1e-8f) & (t >= 0.001f) & (t <= t_best) & inside;
         t_best = ok ? t : t_best;
         best = ok ? (int32_t)k : best;
     }
@@ -610,95 +749,8 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     uint32_t k = 0;
     for (uint32_t r = 0; r < sc.n_wruns; ++r) {
         const uint32_t run = runs[r];
-        const uint32_t kind = run & WKIND_MASK, count = run >> WKIND_BITS, end = k + count;
-        if (kind == PRIM_QUAD_X) { axis_quad_run<0>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
-        if (kind == PRIM_QUAD_Y) { axis_quad_run<1>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
-        if (kind == PRIM_QUAD_Z) { axis_quad_run<2>(wp, k, end, ray, inv, oinv, t_best, best); continue; }
-        if (kind == PRIM_ABOX) {  // room: axis-aligned box whose present faces are quads
-            for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
-                const ConstPrimWorld<float> q = wp + k;
-                const uint32_t present = q->meta >> ABOX_PRESENT_SHIFT;
-                const float lx = q->N[0] * inv[0] - oinv[0], hx = q->AB[0] * inv[0] - oinv[0];
-                const float ly = q->N[1] * inv[1] - oinv[1], hy = q->AB[1] * inv[1] - oinv[1];
-                const float lz = q->N[2] * inv[2] - oinv[2], hz = q->AB[2] * inv[2] - oinv[2];
-                const float nx = fminf(lx, hx), ny = fminf(ly, hy), nz = fminf(lz, hz);
-                const float fx = fmaxf(lx, hx), fy = fmaxf(ly, hy), fz = fmaxf(lz, hz);
-                const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
-                // face slots 2*axis + side (branch-free selects): entry slots from the ray's
-                // direction signs, exit = the opposite side of the exit axis
-                uint32_t e = entry_slot[2], x = entry_slot[2] ^ 1u;
-                e = tn == ny ? entry_slot[1] : e;
-                e = tn == nx ? entry_slot[0] : e;
-                x = tf == fy ? entry_slot[1] ^ 1u : x;
-                x = tf == fx ? entry_slot[0] ^ 1u : x;
-                const bool use_entry = (tn >= 0.001f) & (__builtin_amdgcn_ubfe(present, e, 1) != 0u);
-                const float t = use_entry ? tn : tf;
-                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best) & (use_entry | (__builtin_amdgcn_ubfe(present, x, 1) != 0u));
-                t_best = ok ? t : t_best;
-                best = ok ? (int32_t)(k + 1 + (use_entry ? e : x)) : best;  // the face quad's record
-            }
-            continue;
-        }
-        if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
-            for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
-                const ConstPrimWorld<float> q = wp + k;
-                // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
-                const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
-                const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
-                const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
-                const float ix = __builtin_amdgcn_rcpf(lx.x), iy = __builtin_amdgcn_rcpf(ly.x),
-                            iz = __builtin_amdgcn_rcpf(lz.x);
-                const float ax = (q->D - lx.y) * ix, ay = (q->AB[3] - ly.y) * iy, az = (q->AB[7] - lz.y) * iz;
-                const float bx = ax + ix, by = ay + iy, bz = az + iz;  // planes x' = 0 and x' = 1
-                const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                // entry face unless it lies before t_min (origin on or inside the box): then the exit face
-                const bool entry = tn >= 0.001f;
-                const float t = entry ? tn : tf;
-                const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
-                // face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0),
-                // then the quad that lies there (3 bits per slot in meta)
-                const uint32_t sx = ix < 0.0f ? 1u : 0u, sy = iy < 0.0f ? 3u : 2u, sz = iz < 0.0f ? 5u : 4u;
-                uint32_t se = sz, sxit = sz ^ 1u;
-                se = tn == fminf(ay, by) ? sy : se;
-                se = tn == fminf(ax, bx) ? sx : se;
-                sxit = tf == fmaxf(ay, by) ? sy ^ 1u : sxit;
-                sxit = tf == fmaxf(ax, bx) ? sx ^ 1u : sxit;
-                const uint32_t slot = entry ? se : sxit;
-                const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
-                t_best = ok ? t : t_best;
-                best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
-            }
-            continue;
-        }
-        if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres (not compiled in)
-            for (; k < end; ++k) {
-                DPrim<R> sp;
-                for (int c = 0; c < 3; ++c) { sp.a[c] = wp[k].N[c]; sp.b[c] = wp[k].AB[c]; }
-                sp.s = wp[k].D;
-                const float t = sphere_t(sp, ray);
-                const bool ok = (t >= 0.0f) & (t <= t_best);
-                t_best = ok ? t : t_best;
-                best = ok ? (int32_t)k : best;
-            }
-            continue;
-        }
-        const bool quad = kind == PRIM_QUAD;
-        for (; k < end; ++k) {
-            const ConstPrimWorld<float> q = wp + k;
-            const f32x2 dn = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];  // (N.d, N.o)
-            const float t = (q->D - dn.y) * __builtin_amdgcn_rcpf(dn.x);
-            const float px = ray.o.x + t * ray.d.x, py = ray.o.y + t * ray.d.y, pz = ray.o.z + t * ray.d.z;
-            const f32x2 ab = f32x2{q->AB[0], q->AB[1]} * px + f32x2{q->AB[2], q->AB[3]} * py +
-                             f32x2{q->AB[4], q->AB[5]} * pz - f32x2{q->AB[6], q->AB[7]};  // (alpha, beta)
-            const float lo = fminf(ab.x, ab.y);
-            // quad closed [0,1]^2 (plane.rs:121-126), triangle open (plane.rs:128-133); a NaN
-            // coordinate can only come from a rejected denominator or t
-            const bool inside = quad ? (lo >= 0.0f) & (ab.x <= 1.0f) & (ab.y <= 1.0f) : (lo > 0.0f) & (ab.x + ab.y < 1.0f);
-            const bool ok = (fabsf(dn.x) >= 1e-8f) & (t >= 0.001f) & (t <= t_best) & inside;
-            t_best = ok ? t : t_best;
-            best = ok ? (int32_t)k : best;
-        }
+        const uint32_t kind = run & WRUN_KIND_MASK, count = run >> WRUN_KIND_BITS;
+        world_run<FLAT>(wp, kind, k, count, ray, dox, doy, doz, inv, oinv, entry_slot, t_best, best);
     }
     hm.t = t_best;
     hm.prim = (uint32_t)best;
@@ -712,7 +764,7 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
 // lane's stack (LDS, entry k at stack[k * BLOCK]), so t_best shrinks early and
 // culls the far side.  The lanes of a wave descend until each holds a leaf (or
 // is done) before leaves are tested together ("while-while").
-template <bool FLAT = false>
+template <bool FLAT = false, bool TIE = false>
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
     const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
     if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres
@@ -731,8 +783,9 @@ __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const 
     const float lo = fminf(alpha, beta);
     const bool inside = kind == PRIM_QUAD ? (lo >= 0.0f) & (alpha <= 1.0f) & (beta <= 1.0f)
                                           : (lo > 0.0f) & (alpha + beta < 1.0f);
-    const bool ok = (fabsf(denom) >= 1e-8f) & (t >= 0.001f) & (t <= t_best) & inside;
-    return ok ? t : -1.0f;
+    const float key = tie_key<TIE>(t, tie_factor(q.meta >> WCLASS_SHIFT));  // coplanar-tie key
+    const bool ok = (fabsf(denom) >= 1e-8f) & (t >= 0.001f) & (key <= t_best) & inside;
+    return ok ? key : -1.0f;
 }
 
 template <typename T>
@@ -771,16 +824,22 @@ __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray
 }
 
 // Test the primitives of leaf `ref` (world_prim_t, closest hit so far in ts).
-template <typename R, bool FLAT>
-__device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
+template <typename R, bool FLAT, bool TIE>
+__device__ __forceinline__ void wbvh_leaf_t(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
     const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
     for (uint32_t k = 0; k < cnt; ++k) {
         const DPrimWorld<float> q = load16(sc.wprims + first + k);
-        const float t = world_prim_t<FLAT>(q, ray, ts.t_best);
+        const float t = world_prim_t<FLAT, TIE>(q, ray, ts.t_best);
         const bool ok = t >= 0.0f;
         ts.t_best = ok ? t : ts.t_best;
         ts.best = ok ? (int32_t)(first + k) : ts.best;
     }
+}
+// t_best holds the closest key; coplanar-tie keys only in scenes that have such pairs
+template <typename R, bool FLAT>
+__device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
+    if (sc.wflags & WFLAG_COPLANAR) wbvh_leaf_t<R, FLAT, true>(ts, sc, ray, ref);
+    else wbvh_leaf_t<R, FLAT, false>(ts, sc, ray, ref);
 }
 
 __device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, const int32_t* stack) {
@@ -1046,7 +1105,12 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
                                                      const HitMin<R, MAXD>& hm) {
     // hm.prim is always a primitive record: box and room hits name their face quad
     const DPrimWorld<R> q = load16(sc.wprims + hm.prim);
-    const V<R> pw = wray.o + hm.t * wray.d;
+    R t = hm.t;  // world BVH: the closest key = t scaled by the winner's coplanar-tie factor (WCLASS_*)
+    if (MAXD < 0 && (sc.wflags & WFLAG_COPLANAR)) {
+        const uint32_t cls = q.meta >> WCLASS_SHIFT;
+        t = cls == WCLASS_WIN ? t * R(1.0 / (1.0 - (double)WTIE_EPS)) : (cls == WCLASS_LOSE ? t * R(1.0 / (1.0 + (double)WTIE_EPS)) : t);
+    }
+    const V<R> pw = wray.o + t * wray.d;
     const uint32_t kind = q.meta & WKIND_MASK;
     Rec<R> h;
     h.p = pw;
@@ -1073,7 +1137,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     const R sign = signum(dot(wray.d, geo));
     h.front = sign < R(0);
     h.n = (-sign) * shade;
-    h.mat = q.meta >> WKIND_BITS;
+    h.mat = (q.meta >> WKIND_BITS) & WMAT_MASK;
     return h;
 }
 

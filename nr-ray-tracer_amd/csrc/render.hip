@@ -45,6 +45,7 @@ struct DeviceScene {
     std::vector<void*> allocations;
     size_t bytes = 0;
     bool world_ok = false;  // fast kernel may run in world-space mode (v32.wprims)
+    bool list_ok = false;   // ... in world-list mode (coplanar ties resolved by order)
     uint64_t world_units = 0;
     bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
     bool perlin = false;    // Noise / Marble textures present (KF_PERLIN kernel variants)
@@ -121,7 +122,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         ds->flat = !ds->perlin;
         for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
         // unit kinds from the runs (box / room units also hold header and empty face slots)
-        for (uint32_t run : fs.wruns) ds->flat &= (run & WKIND_MASK) != PRIM_SPHERE;
+        for (uint32_t run : fs.wruns) ds->flat &= (run & WRUN_KIND_MASK) != PRIM_SPHERE;
         ds->flat &= !fs.wruns.empty();
         ds->wbvh_prims = wbp;
         const size_t qbytes = (size_t)QUEUE_SLOTS * QUEUE_HEADS * QUEUE_STRIDE * sizeof(unsigned int);
@@ -130,6 +131,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         check(hipMemset(ds->queues, 0, qbytes), "hipMemset(queues)");
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();
         ds->world_ok = fs.world_ok;
+        ds->list_ok = fs.list_ok;
         ds->world_units = fs.world_units;
     } catch (...) {
         gpu_free_scene(ds);
@@ -158,9 +160,12 @@ int gpu_scene_device(const DeviceScene* ds) { return ds ? ds->device : -1; }
 int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace) {
     const int inst_maxd = ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1;
     if (trace == NRT_TRACE_BVH) return inst_maxd;
-    const bool world = ds->world_ok && ds->v32.n_wprims > 0;
+    const bool world = ds->world_ok && ds->list_ok && ds->v32.n_wprims > 0;
     if (trace == NRT_TRACE_WORLD_LIST) {
-        if (!world) throw std::invalid_argument("trace=world-list: scene has primitives that cannot be flattened to world space");
+        if (!ds->world_ok || ds->v32.n_wprims == 0)
+            throw std::invalid_argument("trace=world-list: scene has primitives that cannot be flattened to world space");
+        if (!ds->list_ok)
+            throw std::invalid_argument("trace=world-list: coplanar surfaces whose f32 tie the world list cannot resolve");
         return MODE_WORLD_LIST;
     }
     if (trace == NRT_TRACE_WORLD_BVH) {

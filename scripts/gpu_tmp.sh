@@ -1,12 +1,4 @@
-# scratch GPU script (varies per experiment): GPU tests, C4 / C1-big / C5 benches
 set -o pipefail
-mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_pytest.log 2>&1 || { tail -30 gpurun_out/t_pytest.log; exit 1; }
-tail -2 gpurun_out/t_pytest.log
-run() {  # name, args...
-  local name=$1; shift
-  timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/t_$name.json 2> gpurun_out/t_$name.err || { echo "bench $name failed rc=$?"; tail -3 gpurun_out/t_$name.err; return 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'Msamples/s', d['roofline']['kernel_ms'], 'ms')" gpurun_out/t_$name.json $name
-}
-run c4_f32 --scene scenes/utah-teapot-scene.json && run c1_f32_big --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 && run c5_f32
+bash scripts/ab.sh nr-ray-tracer_amd/ab/base/libnrt.so nr-ray-tracer_amd/nrt/libnrt.so 3 || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_stat_parity.py -m gpu -v -s --timeout 300 --timeout-method thread > gpurun_out/r02l_stat.log 2>&1; echo "stat rc=$?"; grep -E "chi2|FAIL|Error" gpurun_out/r02l_stat.log | tail -20
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r02l_gpu.log 2>&1; echo "gpu rc=$?"; tail -5 gpurun_out/r02l_gpu.log

@@ -204,6 +204,11 @@ def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
     s = load(scene, w, h, 1, bounces)
     if trace != "bvh" and s.stats()["world_prims"] == 0:
         pytest.skip("scene does not flatten to world space")
+    if trace == "world-list" and not s.stats()["world_list_ok"]:
+        # coplanar surfaces whose f32 tie the world list cannot order (AUTO takes the world BVH)
+        with pytest.raises(nrt.NrtError):
+            s.render(precision="f32", rng="chacha8", trace=trace)
+        pytest.skip("world list refuses this scene's coplanar ties")
     a = s.render(precision="f32", rng="chacha8", trace=trace)
     b = s.render(precision="f64", rng="chacha8")
     mismatch = np.mean(np.abs(a - b).max(axis=2) > 1e-3 + 1e-3 * np.abs(b).max(axis=2))

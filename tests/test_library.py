@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nrt.lib().nrt_abi_version() == 1
+    assert nrt.lib().nrt_abi_version() == 2
 
 
 def test_camera_builder_default_and_build():
@@ -116,3 +116,23 @@ def test_render_without_gpu_fails_loudly():
     with pytest.raises(nrt.NrtError) as ei:
         scene.render(cam)
     assert ei.value.code == -3
+
+
+@pytest.mark.parametrize("scene,pairs,list_ok", [
+    ("scenes/cornell-box-scene.json", 2, 1),   # both cubes stand on the floor (y = 0)
+    ("scenes/scale.json", 1, 1),
+    ("scenes/cube-scene.json", 2, 0),          # touching cube faces: world BVH keys, not the list
+    ("scenes/utah-teapot-scene.json", 0, 1),
+    ("scenes/spheres.toml", 0, 1),
+])
+def test_coplanar_ties_detected(scene, pairs, list_ok):
+    """Overlapping coplanar surfaces tie exactly in the reference (BVH::hit picks the later
+    candidate, object.rs:109-115); the flattener finds them and keeps the world list only
+    where its f32 formulas tie bit for bit (device_scene.hpp WCLASS_*)."""
+    from helpers import in_golden
+
+    with in_golden():
+        s = nrt.Scene.load(scene, nrt.CameraConfig(width=8, height=8, samples_per_pixel=1))
+    st = s.stats()
+    assert st["coplanar_pairs"] == pairs
+    assert st["world_list_ok"] == list_ok
