@@ -60,6 +60,23 @@ struct DeviceScene {
 };
 constexpr uint32_t QUEUE_SLOTS = 256;
 
+// Makes `device` current for a scope and restores the caller's device afterwards: the
+// library never leaves the caller's (e.g. torch's) current device changed, and every
+// allocation, memset and launch goes to the device the scene lives on.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (device != prev) check(hipSetDevice(device), "hipSetDevice");
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 int gpu_device_count() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -75,7 +92,7 @@ static bool use_wbvh4(const FlatScene& fs) {
 }
 
 DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
-    check(hipSetDevice(device), "hipSetDevice");
+    DeviceGuard guard(device);
     auto* ds = new DeviceScene();
     ds->device = device;
     try {
@@ -180,6 +197,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
                        uint32_t trace, void* stream_ptr) {
     if (p.pixel_end <= p.pixel_begin) return;
     if (p.width == 0) throw std::runtime_error("width must be > 0");
+    DeviceGuard guard(ds->device);  // memset, occupancy query and launch on the scene's device
     hipStream_t stream = (hipStream_t)stream_ptr;
     RenderParams q = p;
     if (rng == RNG_PHILOX) {  // group size and count: launch_variant (launch_impl.hpp)
@@ -224,25 +242,28 @@ void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t coun
 
 namespace nrt {
 void* device_alloc(size_t bytes, int device) {
-    check(hipSetDevice(device), "hipSetDevice");
+    DeviceGuard guard(device);
     void* p = nullptr;
     check(hipMalloc(&p, bytes ? bytes : 16), "hipMalloc(output)");
     return p;
 }
 void device_free(void* p, int device) {
-    (void)hipSetDevice(device);
-    (void)hipFree(p);
+    try {
+        DeviceGuard guard(device);
+        (void)hipFree(p);
+    } catch (...) {
+    }
 }
 void device_copy_to_host(void* dst, const void* src, size_t bytes, int device) {
-    check(hipSetDevice(device), "hipSetDevice");
+    DeviceGuard guard(device);
     check(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy(output)");
 }
 void device_zero(void* p, size_t bytes, int device) {
-    check(hipSetDevice(device), "hipSetDevice");
+    DeviceGuard guard(device);
     check(hipMemset(p, 0, bytes), "hipMemset");
 }
 void device_sync(int device) {
-    check(hipSetDevice(device), "hipSetDevice");
+    DeviceGuard guard(device);
     check(hipDeviceSynchronize(), "render kernel");
 }
 }  // namespace nrt
