@@ -15,6 +15,7 @@ DecodedImage decode_image_file(const std::string& path) {
     std::ifstream f(path, std::ios::binary);
     if (!f) throw std::runtime_error("No such file or directory (os error 2): " + path);
     std::vector<uint8_t> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    data.shrink_to_fit();  // exact allocation: a decoder read past the end is a heap overflow under ASan
     DecodedImage img;
     std::string err;
     if (data.size() >= 3 && data[0] == 0xFF && data[1] == 0xD8) {

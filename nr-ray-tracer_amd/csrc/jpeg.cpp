@@ -400,6 +400,7 @@ struct Decoder {
         while (pos + 4 <= n) {
             if (d[pos] != 0xFF) return fail("marker expected");
             while (pos < n && d[pos] == 0xFF) ++pos;  // fill bytes
+            if (pos >= n) return fail("truncated marker");
             const int m = d[pos++];
             if (m == 0xD9) break;  // EOI
             if (m >= 0xD0 && m <= 0xD7) continue;
