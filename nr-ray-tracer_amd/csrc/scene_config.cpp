@@ -5,7 +5,8 @@
 // `instances` are accepted both in the current `[[id, {Kind: {...}}], ...]`
 // sequence form (scene_config.rs:387-400) and in the legacy TOML table form
 // `[textures.<id>.<Kind>]` used by spheres.toml / earth.toml,
-// keeping document order.
+// keeping document order; the older index-based schema of triangles.toml is
+// normalised onto the current one first (normalize_legacy).
 #include "scene_config.hpp"
 
 #include <algorithm>
@@ -215,6 +216,55 @@ MaterialPtr get_material(const Value* id, const MaterialMap& materials, const Ma
     return it->second;
 }
 
+// The legacy scene schema of scenes/triangles.toml:22-189: `textures`
+// and `materials` are arrays of variant tables referenced by integer index and the
+// objects sit in `objects`.  It maps onto the current schema with ids "0", "1", ...
+// -- the scene `nr-ray-tracer create triangles` now writes with named ids
+// (create/triangles.rs:10-86).  Other documents are returned unchanged.
+Value legacy_refs(const Value& v) {
+    Value out = v;
+    if (v.kind == Value::Table) {
+        for (auto& kv : out.tab) {
+            const std::string& k = kv.first;
+            if ((k == "material" || k == "texture" || k == "even" || k == "odd") && kv.second.kind == Value::Int) {
+                Value id = Value::make(Value::String);
+                id.s = std::to_string(kv.second.i);
+                kv.second = id;
+            } else {
+                kv.second = legacy_refs(kv.second);
+            }
+        }
+    } else if (v.kind == Value::Array) {
+        for (auto& e : out.arr) e = legacy_refs(e);
+    }
+    return out;
+}
+
+Value normalize_legacy(const Value& doc) {
+    if (doc.kind != Value::Table || !doc.get("objects") || doc.get("scene")) return doc;
+    Value out = Value::make(Value::Table);
+    for (const auto& [k, v] : doc.tab) {
+        if (k == "objects") {
+            out.tab.emplace_back("scene", legacy_refs(v));
+        } else if ((k == "textures" || k == "materials") && v.kind == Value::Array &&
+                   std::all_of(v.arr.begin(), v.arr.end(), [](const Value& e) { return e.kind == Value::Table; })) {
+            Value list = Value::make(Value::Array);
+            for (size_t i = 0; i < v.arr.size(); ++i) {
+                Value pair = Value::make(Value::Array);
+                Value id = Value::make(Value::String);
+                id.s = std::to_string(i);
+                pair.arr.push_back(id);
+                pair.arr.push_back(legacy_refs(v.arr[i]));
+                list.arr.push_back(pair);
+            }
+            out.tab.emplace_back(k, list);
+        } else {
+            out.tab.emplace_back(k, v);
+        }
+    }
+    return out;
+}
+
 struct Builder {
     int depth = 0;
 
@@ -326,8 +376,8 @@ struct Builder {
         const size_t dot = path.find_last_of('.');
         const size_t slash = path.find_last_of('/');
         const std::string ext = (dot == std::string::npos || (slash != std::string::npos && dot < slash)) ? "" : path.substr(dot + 1);
-        if (ext == "json") return parse_json(read_file(path));
-        if (ext == "toml") return parse_toml(read_file(path));
+        if (ext == "json") return normalize_legacy(parse_json(read_file(path)));
+        if (ext == "toml") return normalize_legacy(parse_toml(read_file(path)));
         fail("invalid scene file format!");
     }
 };

@@ -372,6 +372,35 @@ class Builder:
         return root, builder
 
 
+_LEGACY_REFS = ("material", "texture", "even", "odd")
+
+
+def _legacy_refs(v: Any) -> Any:
+    """Integer texture / material references of the legacy schema -> the ids normalize_legacy gives."""
+    if isinstance(v, dict):
+        return {k: (str(x) if k in _LEGACY_REFS and isinstance(x, int) and not isinstance(x, bool) else _legacy_refs(x))
+                for k, x in v.items()}
+    if isinstance(v, list):
+        return [_legacy_refs(x) for x in v]
+    return v
+
+
+def normalize_legacy(doc: Any) -> Any:
+    """The legacy scene schema of scenes/triangles.toml:22-189: `textures` and
+    `materials` are arrays of variant tables referenced by integer index and the objects
+    sit in `objects`.  It maps onto the current schema with ids "0", "1", ... -- the scene
+    `nr-ray-tracer create triangles` now writes with named ids (create/triangles.rs:10-86)."""
+    if not isinstance(doc, dict) or "objects" not in doc or "scene" in doc:
+        return doc
+    out = dict(doc)
+    for key in ("textures", "materials"):
+        v = doc.get(key)
+        if isinstance(v, list) and all(isinstance(e, dict) for e in v):
+            out[key] = [[str(i), _legacy_refs(e)] for i, e in enumerate(v)]
+    out["scene"] = _legacy_refs(out.pop("objects"))
+    return out
+
+
 def load_doc(path: str) -> Any:  # scene_config.rs:475-492
     ext = os.path.splitext(path)[1]
     if ext not in (".json", ".toml"):
@@ -381,8 +410,8 @@ def load_doc(path: str) -> Any:  # scene_config.rs:475-492
     with open(path, "rb") as fh:
         raw = fh.read()
     if ext == ".json":
-        return json.loads(raw.decode("utf-8"))
-    return tomli.loads(raw.decode("utf-8"))
+        return normalize_legacy(json.loads(raw.decode("utf-8")))
+    return normalize_legacy(tomli.loads(raw.decode("utf-8")))
 
 
 def build_tree(path: str, overrides: CameraConfig | None, texel_dir: str) -> tuple[str, CameraBuilder]:

@@ -1,2 +1,2 @@
 set -o pipefail
-timeout -k 10 400 python -u -m pytest tests/test_multigpu.py -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/r02m_mgpu.log 2>&1; echo "mgpu rc=$?"; tail -15 gpurun_out/r02m_mgpu.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r02n_gpu.log 2>&1; echo "gpu rc=$?"; tail -12 gpurun_out/r02n_gpu.log

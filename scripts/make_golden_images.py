@@ -30,6 +30,8 @@ CASES = {
     "quads": ("scenes/quads.toml", 32, 32, 4, None),
     "teapot": ("scenes/utah-teapot-scene.json", 32, 24, 2, None),
     "earth": ("scenes/earth.toml", 48, 27, 2, None),
+    "triangles": ("scenes/triangles.toml", 40, 30, 4, None),
+    "checker": ("scenes/checker.json", 48, 32, 4, None),
 }
 # files each scene reads (scene file, models it references, textures)
 INPUTS = {

@@ -33,6 +33,8 @@ CASES_F64 = [
     ("scenes/earth.toml", 48, 27, 2, None),               # image textures (JPEG), r = 1000 ground sphere
     ("scenes/noise.toml", 40, 30, 2, None),               # Perlin Noise + Marble textures (parity unpinned)
     ("scenes/simple-lights.toml", 40, 30, 2, None),       # Marble + emissive quad / sphere
+    ("scenes/triangles.toml", 40, 30, 4, None),           # legacy index schema (Q14)
+    ("scenes/checker.json", 48, 32, 4, None),             # Checker: nested, default, negative, 1e20 scales
 ]
 
 

@@ -27,6 +27,8 @@ LOADABLE = [
     ("scenes/earth.toml", dict(width=64, height=36, spp=2)),              # two 2048x1024 JPEG textures
     ("scenes/noise.toml", dict(width=40, height=30, spp=2)),              # Perlin Noise + Marble textures
     ("scenes/simple-lights.toml", dict(width=40, height=30, spp=2)),      # Marble + lights
+    ("scenes/triangles.toml", dict(width=40, height=30, spp=2)),          # legacy index schema (Q14)
+    ("scenes/checker.json", dict(width=40, height=30, spp=2)),            # Checker textures (test scene)
 ]
 
 
@@ -94,8 +96,47 @@ def test_spheres_counts():
     assert st["instances"] == 0
 
 
+# `nr-ray-tracer create triangles` (create/triangles.rs:10-117) in the current schema: the same
+# scene as the legacy scenes/triangles.toml, with named ids instead of indices (and the file's
+# +0.0 where today's 4.0 * DVec3::NEG_Z would write -0.0)
+TRIANGLES_CURRENT = """{
+ "camera": {"background_color": [0.7, 0.8, 1.0], "look_from": [0.0, 0.0, 9.0], "look_at": [0.0, 0.0, 0.0],
+            "field_of_view": 80.0, "ray_max_bounces": 10, "samples_per_pixel": 10},
+ "textures": [["solid_red", {"SolidColor": {"color": [1.0, 0.2, 0.2]}}],
+              ["solid_green", {"SolidColor": {"color": [0.2, 1.0, 0.2]}}],
+              ["solid_blue", {"SolidColor": {"color": [0.2, 0.2, 1.0]}}],
+              ["solid_orange", {"SolidColor": {"color": [1.0, 0.5, 0.0]}}],
+              ["solid_cyan", {"SolidColor": {"color": [0.2, 0.8, 0.8]}}]],
+ "materials": [["lambertian_red", {"Lambertian": {"texture": "solid_red"}}],
+               ["lambertian_green", {"Lambertian": {"texture": "solid_green"}}],
+               ["lambertian_blue", {"Lambertian": {"texture": "solid_blue"}}],
+               ["lambertian_orange", {"Lambertian": {"texture": "solid_orange"}}],
+               ["lambertian_cyan", {"Lambertian": {"texture": "solid_cyan"}}]],
+ "scene": [
+  {"Triangle": {"point": [-3.0, -2.0, 5.0], "u": [0.0, 0.0, -4.0], "v": [0.0, 4.0, 0.0], "material": "lambertian_red"}},
+  {"Triangle": {"point": [-2.0, -2.0, 0.0], "u": [4.0, 0.0, 0.0], "v": [0.0, 4.0, 0.0], "material": "lambertian_green"}},
+  {"Triangle": {"point": [3.0, -2.0, 1.0], "u": [0.0, 0.0, 4.0], "v": [0.0, 4.0, 0.0], "material": "lambertian_blue"}},
+  {"Triangle": {"point": [-2.0, 3.0, 1.0], "u": [4.0, 0.0, 0.0], "v": [0.0, 0.0, 4.0], "material": "lambertian_orange"}},
+  {"Triangle": {"point": [-2.0, -3.0, 5.0], "u": [4.0, 0.0, 0.0], "v": [0.0, 0.0, -4.0], "material": "lambertian_cyan"}}
+ ]
+}"""
+
+
+def test_legacy_triangles_equal_current_schema(tmp_path):
+    """scenes/triangles.toml (index-based legacy schema, triangles.toml:22-189) loads as the scene
+    today's `create triangles` writes (create/triangles.rs): identical canonical dumps."""
+    cur = tmp_path / "triangles-current.json"
+    cur.write_text(TRIANGLES_CURRENT)
+    ov = dict(width=40, height=30, spp=2)
+    legacy, _ = product_dump("scenes/triangles.toml", ov)
+    current, _ = product_dump(str(cur), ov)
+    assert _norm(legacy) == _norm(current)
+    with tempfile.TemporaryDirectory() as td:  # and the oracle's independent loader agrees
+        tree, _ = oracle_tree(str(cur), td, width=40, height=30, spp=2)
+        assert _norm(oracle_dump(tree)) == _norm(current)
+
+
 @pytest.mark.parametrize("scene,code", [
-    ("scenes/triangles.toml", -2),           # legacy schema (Q14)
     ("scenes/does-not-exist.json", -2),
     ("scenes/textures/earth.jpg", -2),       # not a scene format
 ])
