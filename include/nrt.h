@@ -29,7 +29,7 @@ enum {
     NRT_E_INVALID = -1,     /* bad argument */
     NRT_E_LOAD = -2,        /* scene file / config error (anyhow::Error in the reference) */
     NRT_E_DEVICE = -3,      /* HIP error / no device */
-    NRT_E_UNSUPPORTED = -4  /* feature outside the accelerated path (e.g. Perlin textures) */
+    NRT_E_UNSUPPORTED = -4  /* feature outside the accelerated path (reserved; every reference scene feature renders) */
 };
 
 enum nrt_precision { NRT_PRECISION_F64 = 0, NRT_PRECISION_F32 = 1 };
@@ -146,7 +146,7 @@ int nrt_camera_build(const nrt_camera_builder* b, nrt_camera* out);  /* CameraBu
 int nrt_camera_config_apply(const nrt_camera_config* cfg, nrt_camera_builder* b);
 
 /* ---- scene from file: SceneConfig::try_load_scene + merge_with + try_build
- *      (app scene_config.rs:475-496, render.rs:556-560).  Relative paths inside
+ *      (app scene_config.rs:475-496, render.rs:107-111).  Relative paths inside
  *      the file (nested scenes, textures) resolve against the process CWD, as in
  *      the reference.  `overrides` may be NULL. */
 int nrt_scene_load(const char* path, const nrt_camera_config* overrides, nrt_scene** out, nrt_camera* camera);

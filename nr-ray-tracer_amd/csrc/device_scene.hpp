@@ -10,10 +10,10 @@
 //     reference's candidate order, so "the later candidate wins ties"
 //     reproduces `if hit_l.t < hit_r.t {l} else {r}` (object.rs:109-115).
 //   * primitives (sphere / quad / triangle) with the PlaneBuilder
-//     precomputation (plane.rs:381-413),
+//     precomputation (plane.rs:95-128),
 //   * instances = a chain of Translate/Rotate/Scale applied outer -> inner to
 //     the ray, inner -> outer to the hit point/normal (translate.rs:37-49,
-//     rotate.rs:141-156, scale.rs:230-243), plus the BLAS root,
+//     rotate.rs:91-106, scale.rs:73-86), plus the BLAS root,
 //   * materials and textures (image texels as f32 RGB, row-major).
 // Layout is precision-templated: Real = double for the reference-exact
 // kernel, float for the fast kernel.  Nothing here is torch-aware.

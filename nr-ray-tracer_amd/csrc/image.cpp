@@ -1,5 +1,5 @@
 // Image texture decoding: ImageReader::open(path)?.decode()?.into_rgb32f()
-// (lib/textures/image.rs:76-80).  Baseline JPEG is decoded by jpeg.cpp.
+// (lib/textures/image.rs:23-27).  Baseline JPEG is decoded by jpeg.cpp.
 #include <cstdio>
 #include <fstream>
 #include <sstream>

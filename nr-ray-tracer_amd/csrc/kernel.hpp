@@ -503,7 +503,7 @@ struct Rec {  // HitRecord (hitable.rs:14-22) of the closest hit, world space
     uint32_t mat;
 };
 
-// hit point / normal back out (inner -> outer); Scale leaves the normal alone (scale.rs:239-242)
+// hit point / normal back out (inner -> outer); Scale leaves the normal alone (scale.rs:82-85)
 template <typename R>
 __device__ __forceinline__ void xform_out(const DSceneView<R>& sc, const DInstance& inst, Rec<R>& h) {
     for (uint32_t k = inst.num_xforms; k-- > 0;) {
@@ -1283,7 +1283,7 @@ __device__ __forceinline__ double perlin_texture(const float* texels, const DTex
     return t.kind == TEX_NOISE ? n : (1.0 + sin(t.color[0] * pz + 10.0 * n)) / 2.0;
 }
 
-// Texture::get_color (solid_color.rs:45-53, image.rs:83-94, checker.rs:170-184,
+// Texture::get_color (solid_color.rs:35-43, textures/image.rs:31-40, checker.rs:76-89,
 // noise.rs:136-144, marble.rs:87-96); `p` = the world-space hit point
 template <typename R, bool PERLIN>
 __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> p) {
@@ -1515,7 +1515,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         }
         h = make_record<R, MAXD, EXACT, FLAT>(sc, ray, hm);
         m = material(h.mat);
-        if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:131-143), no scatter
+        if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:62-75), no scatter
             const R k = bounced ? m.param : R(1.0);
             contrib = tp * (k * albedo(m, h));
             return false;

@@ -120,7 +120,7 @@ V3 m4_transform_vector3(const M4& m, V3 r) {
 
 // ------------------------------------------------------------------- AABB
 static Interval pad_axis(Interval a) {
-    const double eps = 0.0001;  // AABB::EPSILON (aabb.rs:241)
+    const double eps = 0.0001;  // AABB::EPSILON (aabb.rs:14)
     const double size = a.max - a.min;
     if (size < eps) {
         const double padding = (eps - size) / 2.;

@@ -3,9 +3,9 @@
 // built with the reference's exact f64 arithmetic before flattening.
 //
 //   lib/objects/object.rs:40-121   BVH (median split, un-narrowed hit, ties -> right)
-//   lib/objects/sphere.rs:191-213  Sphere bbox
-//   lib/objects/plane.rs:381-413   Plane precompute (normal, d, w, bbox)
-//   lib/objects/translate.rs:18-30, rotate.rs:63-112, scale.rs:167-215  transform bboxes
+//   lib/objects/sphere.rs:69-92  Sphere bbox
+//   lib/objects/plane.rs:95-128   Plane precompute (normal, d, w, bbox)
+//   lib/objects/translate.rs:18-30, rotate.rs:46-106, scale.rs:43-86  transform bboxes
 //   lib/aabb.rs:13-132, lib/interval.rs:10-94  AABB / Interval
 //   lib/camera.rs:94-159           CameraBuilder::build
 //
@@ -68,7 +68,7 @@ struct AABB {
     static AABB empty() { return {{INFINITY, -INFINITY}, {INFINITY, -INFINITY}, {INFINITY, -INFINITY}}; }
     const Interval& axis(int i) const { return i == 0 ? x : i == 1 ? y : z; }
 };
-AABB aabb_new(Interval x, Interval y, Interval z);  // pads thin axes (aabb.rs:243-267)
+AABB aabb_new(Interval x, Interval y, Interval z);  // pads thin axes (aabb.rs:14-40)
 AABB aabb_union(const AABB& a, const AABB& b);
 AABB aabb_from_points(V3 a, V3 b);
 int aabb_longest_axis(const AABB& b);
@@ -78,7 +78,7 @@ int total_cmp(double a, double b);  // f64::total_cmp as -1/0/1
 struct Texture {
     enum Kind { Solid, Image, Checker, Noise, Marble } kind = Solid;
     V3 color{1, 1, 1};
-    // Image: Rgb32F texels (decoded u8/255, no sRGB linearisation, image.rs:76-80)
+    // Image: Rgb32F texels (decoded u8/255, no sRGB linearisation, textures/image.rs:23-27)
     uint32_t width = 0, height = 0;
     std::shared_ptr<std::vector<float>> texels;
     std::shared_ptr<Texture> even, odd;

@@ -135,7 +135,7 @@ TexturePtr make_texture(const Value& cfg, const TextureMap& textures) {
         t->texels = std::make_shared<std::vector<float>>(std::move(img.rgb));
     } else if (kind == "Checker") {
         t->kind = Texture::Checker;
-        auto even = std::make_shared<Texture>();  // CheckerBuilder defaults (checker.rs:145-151)
+        auto even = std::make_shared<Texture>();  // CheckerBuilder defaults (checker.rs:53-59)
         even->color = v3(1, 1, 1);
         auto odd = std::make_shared<Texture>();
         odd->color = v3(0, 0, 0);
@@ -406,7 +406,7 @@ void CameraConfig::try_update(CameraBuilder& b) const {
     switch (key) {
         case 0: break;
         case 6: b.width = width; b.height = height; break;
-        case 5: {  // ImageSize::from_width_and_aspect_ratio (image.rs:210-216)
+        case 5: {  // ImageSize::from_width_and_aspect_ratio (image.rs:26-32)
             double h = (double)width / aspect_ratio;
             uint64_t hh = (h != h || h <= 0) ? 0 : (h >= 18446744073709551615.0 ? UINT64_MAX : (uint64_t)h);
             b.width = width; b.height = hh < 1 ? 1 : hh;

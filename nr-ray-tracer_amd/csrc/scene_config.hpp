@@ -31,7 +31,7 @@ struct LoadedScene {
     Camera camera;
 };
 
-// SceneConfig::try_load_scene + merge_with(cli) + try_build  (render.rs:556-560)
+// SceneConfig::try_load_scene + merge_with(cli) + try_build  (render.rs:107-111)
 LoadedScene load_scene_file(const std::string& path, const CameraConfig* cli_overrides);
 
 // Decoded Rgb32F image (u8/255 per channel), ImageReader::decode().into_rgb32f().

@@ -9,9 +9,9 @@
 //
 // Reference (packages/ray-tracer-lib/src/, read-only at /root/reference):
 //   camera.rs:94-159 (build), 236-267 (get_ray), 269-300 (get_ray_color), 302-343 (render)
-//   vector.rs:27-81  objects/object.rs:40-121  objects/sphere.rs:191-285
-//   objects/plane.rs:309-460  objects/translate.rs:17-50  objects/rotate.rs:63-157
-//   objects/scale.rs:167-244  aabb.rs:13-132  interval.rs:10-94  hitable.rs:37-77
+//   vector.rs:27-81  objects/object.rs:40-121  objects/sphere.rs:69-163
+//   objects/plane.rs:23-30, 95-174  objects/translate.rs:17-50  objects/rotate.rs:13-106
+//   objects/scale.rs:10-86  aabb.rs:13-132  interval.rs:10-94  hitable.rs:37-77
 //   materials/*.rs  textures/{solid_color,image,checker,noise,marble}.rs
 // Third-party arithmetic restated from the pinned crates (Cargo.lock):
 //   rand_core 0.9.3 seed_from_u64 (PCG32), rand_chacha 0.9.0 ChaCha8 BlockRng,

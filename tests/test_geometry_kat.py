@@ -5,7 +5,7 @@ angle every primary ray starts at look_from, so the primary ray of pixel (x, y) 
 closed-form (CameraBuilder::build camera.rs:94-159, get_ray camera.rs:244-267).
 With ray_max_bounces = 1 a pixel of the Cornell box is the light's emission when the
 primary ray's nearest hit is the light quad (DiffuseLight::emit on a ray whose bounce
-flag is 0 gives 1 x the white texture, diffuse_light.rs:131-143; Q4), and black
+flag is 0 gives 1 x the white texture, diffuse_light.rs:62-75; Q4), and black
 otherwise: a scattered ray meets the depth cap (Q6), a miss sees the black background.
 The expected image is computed here in numpy from the scene file's numbers (the light
 sits 0.002 below the ceiling and above both blocks, so no other surface comes first),
