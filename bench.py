@@ -206,6 +206,9 @@ def main():
                     help="f32 kernel traversal (nrt_trace): auto = world-space list for small flattenable scenes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)
+    ap.add_argument("--kernel-only", action="store_true",
+                    help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
+                         "sampled over a render dispatch see the render kernel alone")
     args = ap.parse_args()
 
     import torch
@@ -259,7 +262,7 @@ def main():
         slot = k % 2
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         target = rbuf[slot % len(rbuf)]
-        if world == 1 and copied[slot] is not None:
+        if world == 1 and lead and copied[slot] is not None:
             stream.wait_event(copied[slot])  # render target `slot` was copied out two frames ago
         e0.record(stream)
         scene.render_device(target.data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng, device=local,
@@ -272,7 +275,7 @@ def main():
             if lead and copied[slot] is not None:
                 stream.wait_event(copied[slot])  # frame buffer `slot` was copied out two frames ago
             shard.gather_frame(buf, H, dist, rank, world, out=fr)
-        if lead:
+        if lead and not args.kernel_only:
             ready = torch.cuda.Event()
             ready.record(stream)
             copy_stream.wait_event(ready)
@@ -307,7 +310,7 @@ def main():
 
     if lead:
         last = host[(args.warmup + args.steps - 1) % 2].numpy()
-        frame_sha = hashlib.sha256(last.tobytes()).hexdigest()
+        frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
         samples = float(W) * H * spp
         value = samples * args.steps / elapsed / 1e6
         st = scene.stats()
@@ -334,8 +337,10 @@ def main():
                        "rng": args.rng, "precision": args.precision, "trace": args.trace,
                        "world_prims": st["world_prims"],
                        "parallelism": f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
-                       "timed_step": "render + (N>1) gather/un-permute + device-to-host copy of the frame "
-                                     "(pinned, double-buffered: frame k's copy overlaps frame k+1's render)"},
+                       "timed_step": "render + (N>1) gather/un-permute" + (
+                           " (--kernel-only diagnostics: no device-to-host copy)" if args.kernel_only else
+                           " + device-to-host copy of the frame (pinned, double-buffered: frame k's copy overlaps "
+                           "frame k+1's render)")},
             "roofline": {
                 "bound": "valu", "achieved": None if achieved is None else round(achieved, 3), "peak": peak,
                 "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / peak, 4),
@@ -348,7 +353,8 @@ def main():
                         "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
                         "traffic": traffic},
                 "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
-                                                "wait_inst_frac", "source")} if pmc else None,
+                                                "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
+                                                "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
                 "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
                         "divergence; its HBM traffic is the framebuffer plus a few KB of scene"},
             "work": work_block(wc, value, args.precision),

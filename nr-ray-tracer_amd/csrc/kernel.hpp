@@ -31,6 +31,9 @@ constexpr int BLOCK = 256;
 #ifndef NRT_SPECULATIVE
 #define NRT_SPECULATIVE 1  // world-BVH rounds: lanes holding a leaf keep descending (Aila & Laine)
 #endif
+#ifndef NRT_WBVH_IFIF
+#define NRT_WBVH_IFIF 0  // world BVH: one node visit or one primitive per lane and trip (wbvh_trip)
+#endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 
 template <typename R>
@@ -823,11 +826,27 @@ __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray
     ts.best = -1;
 }
 
+// PROF builds (diagnostics only): traversal event counters in the wave's LDS profile row
+// (slots PROF_*), added by the first active lane.
+constexpr int NPROF = 16;
+enum : int { PROF_VISIT_TRIPS = 8, PROF_VISIT_LANES = 9, PROF_LEAF_TRIPS = 10, PROF_LEAF_LANES = 11,
+             PROF_ROUNDS = 12, PROF_ROUND_LANES = 13 };
+__device__ __forceinline__ void prof_event(unsigned long long* pc, int trips, int lanes) {
+    if (!pc) return;
+    const uint64_t m = __ballot(true);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x) {
+        atomicAdd(pc + trips, 1ull);
+        atomicAdd(pc + lanes, (unsigned long long)__popcll(m));
+    }
+}
+
 // Test the primitives of leaf `ref` (world_prim_t, closest hit so far in ts).
 template <typename R, bool FLAT, bool TIE>
-__device__ __forceinline__ void wbvh_leaf_t(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
+__device__ __forceinline__ void wbvh_leaf_t(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref,
+                                            unsigned long long* pc = nullptr) {
     const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
     for (uint32_t k = 0; k < cnt; ++k) {
+        prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
         const DPrimWorld<float> q = load16(sc.wprims + first + k);
         const float t = world_prim_t<FLAT, TIE>(q, ray, ts.t_best);
         const bool ok = t >= 0.0f;
@@ -837,9 +856,10 @@ __device__ __forceinline__ void wbvh_leaf_t(WbvhTrav& ts, const DSceneView<R>& s
 }
 // t_best holds the closest key; coplanar-tie keys only in scenes that have such pairs
 template <typename R, bool FLAT>
-__device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref) {
-    if (sc.wflags & WFLAG_COPLANAR) wbvh_leaf_t<R, FLAT, true>(ts, sc, ray, ref);
-    else wbvh_leaf_t<R, FLAT, false>(ts, sc, ray, ref);
+__device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t ref,
+                                          unsigned long long* pc = nullptr) {
+    if (sc.wflags & WFLAG_COPLANAR) wbvh_leaf_t<R, FLAT, true>(ts, sc, ray, ref, pc);
+    else wbvh_leaf_t<R, FLAT, false>(ts, sc, ray, ref, pc);
 }
 
 __device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, const int32_t* stack) {
@@ -918,7 +938,7 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
 // descending until every lane of the wave has a leaf.
 template <typename R, bool WIDE, bool FLAT>
 __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                                int32_t* stack) {
+                                                int32_t* stack, unsigned long long* pc) {
 #if NRT_SPECULATIVE
     while (true) {
         if (ts.node < 0 && ts.node != WBVH_DONE && ts.leaf == WBVH_NO_LEAF) {  // park a leaf
@@ -929,12 +949,13 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
         if (!__any(inner)) break;                                         // nobody can descend
         if (__all(ts.leaf != WBVH_NO_LEAF || ts.node == WBVH_DONE)) break;  // every lane has a leaf (or is done)
         if (inner) {
+            prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
             if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
             else wbvh2_visit(ts, sc, stack);
         }
     }
     if (ts.leaf != WBVH_NO_LEAF) {
-        wbvh_leaf<R, FLAT>(ts, sc, ray, ts.leaf);
+        wbvh_leaf<R, FLAT>(ts, sc, ray, ts.leaf, pc);
         ts.leaf = WBVH_NO_LEAF;
     }
 #else
@@ -948,15 +969,49 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
 #endif
 }
 
+// "If-if" trip (NRT_WBVH_IFIF): every busy lane does exactly one unit of work per trip,
+// one primitive of its current leaf or, without a leaf, one node visit; a leaf that a visit
+// or a pop turns up becomes the lane's leaf cursor at once (the leaf ref, advanced in place:
+// first + 1, count - 1).  Lanes never wait for the wave to finish a phase, so long and
+// short traversals, and leaves of different sizes, interleave across trips.
+template <typename R, bool WIDE, bool FLAT, bool TIE>
+__device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                               int32_t* stack, unsigned long long* pc) {
+    if (ts.leaf != WBVH_NO_LEAF) {
+        prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
+        const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
+        const DPrimWorld<float> q = load16(sc.wprims + first);
+        const float t = world_prim_t<FLAT, TIE>(q, ray, ts.t_best);
+        const bool ok = t >= 0.0f;
+        ts.t_best = ok ? t : ts.t_best;
+        ts.best = ok ? (int32_t)first : ts.best;
+        ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+    } else if (ts.node >= 0) {
+        prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
+        if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
+        else wbvh2_visit(ts, sc, stack);
+    }
+    if (ts.leaf == WBVH_NO_LEAF && ts.node < 0 && ts.node != WBVH_DONE) {  // a leaf turned up: its cursor
+        ts.leaf = ts.node;
+        ts.node = wbvh_pop(ts, stack);
+    }
+}
+template <typename R, bool WIDE, bool FLAT>
+__device__ __forceinline__ void wbvh_trip(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
+                                          int32_t* stack, unsigned long long* pc) {
+    if (sc.wflags & WFLAG_COPLANAR) wbvh_trip_impl<R, WIDE, FLAT, true>(ts, sc, ray, stack, pc);
+    else wbvh_trip_impl<R, WIDE, FLAT, false>(ts, sc, ray, stack, pc);
+}
+
 template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                           int32_t* stack) {
-    wbvh_round_impl<R, false, FLAT>(ts, sc, ray, stack);
+                                           int32_t* stack, unsigned long long* pc) {
+    wbvh_round_impl<R, false, FLAT>(ts, sc, ray, stack, pc);
 }
 template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh4_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                            int32_t* stack) {
-    wbvh_round_impl<R, true, FLAT>(ts, sc, ray, stack);
+                                            int32_t* stack, unsigned long long* pc) {
+    wbvh_round_impl<R, true, FLAT>(ts, sc, ray, stack, pc);
 }
 
 // Root and round of the tree the scene carries (4-wide when its stack bound fits).
@@ -965,9 +1020,15 @@ __device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
     return sc.wbvh4 ? sc.wbvh4_root : sc.wbvh_root;
 }
 template <typename R, bool FLAT = false>
-__device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack) {
-    if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack);
-    else wbvh_round<R, FLAT>(ts, sc, ray, stack);
+__device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack,
+                                          unsigned long long* pc = nullptr) {
+#if NRT_WBVH_IFIF
+    if (sc.wbvh4) wbvh_trip<R, true, FLAT>(ts, sc, ray, stack, pc);
+    else wbvh_trip<R, false, FLAT>(ts, sc, ray, stack, pc);
+#else
+    if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack, pc);
+    else wbvh_round<R, FLAT>(ts, sc, ray, stack, pc);
+#endif
 }
 
 template <typename R, int MAXD, bool FLAT = false>
@@ -989,8 +1050,16 @@ __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const R
 // so `t <= t_best` (the later candidate wins a tie) reproduces BVH::hit's
 // `if l.t < r.t {l} else {r}` (object.rs:109-115).  Only (t, prim, instance
 // path) is kept; the winner's record is rebuilt afterwards (make_record).
+//
+// `all` (RenderParams::exact_all, small scenes): no box is tested.  BVH::hit tests every
+// primitive whose boxes the ray hits, with the same range on both sides, and keeps the
+// smaller t, ties to the right (object.rs:89-121); boxes are padded (aabb.rs:14-40), so a
+// primitive the ray hits lies in boxes the ray hits, and the closest hit over ALL primitives
+// in depth-first order with `t <= t_best` is the reference's.  Every lane then walks the
+// same node sequence: uniform control flow, broadcast reads.
 template <typename R, int MAXD, bool EXACT>
-__device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
+                                          bool all = false) {
     R t_best = R(INFINITY);
     bool found = false;
     int32_t node = sc.root;
@@ -1010,7 +1079,7 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
             meta = n.meta;
             skip = n.skip;
             if ((meta & 3u) != NODE_INNER) break;
-            node = box_hit<R, EXACT>(n.bmin, n.bmax, ray, t_best) ? node + 1 : skip;
+            node = (all || box_hit<R, EXACT>(n.bmin, n.bmax, ray, t_best)) ? node + 1 : skip;
         }
         if (node < 0) {
             if (depth == 0) break;
@@ -1090,10 +1159,10 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 
 template <typename R, int MAXD, bool EXACT, bool FLAT = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                      int32_t* stack) {
+                                      int32_t* stack, bool all = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
-    else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm);
+    else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
 
 // HitRecord of the winner (HitRecord::new_with_uv, hitable.rs:38-59).
@@ -1398,6 +1467,23 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // (no f64 sphere test, uv mapping or texture lookup compiled in: the Cornell box).
 constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4;
 
+// Philox sample pool: LDS slots per wave (a power of two; see the Philox branch of
+// render_kernel) and the pool's LDS bytes per workgroup for P pixels per group.
+#ifndef NRT_SLOTS_LIST
+#define NRT_SLOTS_LIST 2
+#endif
+#ifndef NRT_SLOTS_BVH
+#define NRT_SLOTS_BVH 4
+#endif
+template <int MAXD>
+constexpr uint32_t philox_slots() {
+    return MAXD == 0 ? NRT_SLOTS_LIST : NRT_SLOTS_BVH;
+}
+template <int MAXD>
+__host__ __device__ constexpr uint32_t philox_pool_bytes(uint32_t P) {
+    return (BLOCK / 64) * philox_slots<MAXD>() * P * (3u * (uint32_t)sizeof(double) + 4u);
+}
+
 template <typename R, class G, int MAXD>
 constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WORLD_LIST_WAVES
@@ -1406,6 +1492,10 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_FLAT_WAVES
 #define NRT_FLAT_WAVES NRT_WORLD_LIST_WAVES
 #endif
+#ifndef NRT_F64_WAVES
+#define NRT_F64_WAVES 4  // f64 kernels: 4 waves per SIMD (C5 410 -> 274 ms, C4 248 -> 158 ms; 3, 5, 6 slower)
+#endif
+    if (sizeof(R) == 8) return NRT_F64_WAVES;
     if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT)) return NRT_FLAT_WAVES;
     return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
 }
@@ -1437,9 +1527,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
     // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
-    __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][8];
+    __shared__ unsigned long long prof[PROF ? BLOCK / 64 : 1][NPROF];
     if constexpr (PROF) {
-        if (threadIdx.x < (BLOCK / 64) * 8) prof[threadIdx.x / 8][threadIdx.x % 8] = 0;
+        if (threadIdx.x < (BLOCK / 64) * NPROF) prof[threadIdx.x / NPROF][threadIdx.x % NPROF] = 0;
         __syncthreads();
     }
     const uint32_t wave = threadIdx.x / 64;
@@ -1450,7 +1540,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     auto flush_prof = [&]() {
         if constexpr (PROF) {
             if (leader()) {
-                for (int c = 0; c < 8; ++c)
+                for (int c = 0; c < NPROF; ++c)
                     if (c != 4) atomicAdd(&p.counters[c], prof[wave][c]);
                 atomicAdd(&p.counters[4], 1ull);
             }
@@ -1458,7 +1548,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     };
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
-    const uint32_t acc_bytes = G::exact_stream ? 0u : (BLOCK / 64) * 2u * p.wave_pixels * (3u * (uint32_t)sizeof(double) + 4u);
+    const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
     constexpr uint32_t stack_bytes = MAXD < 0 ? WBVH_STACK * BLOCK * sizeof(int32_t) : 0;
     int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
@@ -1678,7 +1768,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
-                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);
@@ -1702,21 +1792,29 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     } else {
         // ------------------------------------------------ Philox: per-wave sample pool
         // Persistent waves.  A wave takes groups of P consecutive pixels from a global
-        // queue (one atomic per group) into a ring of two LDS slots and hands the
+        // queue (one atomic per group) into a ring of NS LDS slots and hands the
         // P x spp samples of a group (index s * P + j; pixels past the end of the launch
         // are padding samples that end at once) to whichever lane is free.  A group's
-        // pixel sums are written out when its last sample finishes.
+        // pixel sums are written out when its last sample finishes; the next group goes
+        // into the slot after the one being claimed from, which must have been flushed:
+        // with two slots one long path of the previous group starves the wave's lanes
+        // (world BVH: long and short paths mix), so the BVH modes keep four.
+        constexpr uint32_t NS = philox_slots<MAXD>();
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
         const uint32_t GS = P * p.spp;  // samples per group (host: < 2^32)
-        // LDS per wave: 2 slots x P pixel sums (3 x f64) and 2 x P packed coordinates x | y << 16
-        double* acc = (double*)(lds + ring_bytes) + wv * 2u * P * 3u;
-        uint32_t* slot_xy = (uint32_t*)(lds + ring_bytes + (BLOCK / 64) * 2u * P * 3u * sizeof(double)) + wv * 2u * P;
+        // LDS per wave: NS slots x P pixel sums (3 x f64) and NS x P packed coordinates x | y << 16
+        double* acc = (double*)(lds + ring_bytes) + wv * NS * P * 3u;
+        uint32_t* slot_xy = (uint32_t*)(lds + ring_bytes + (BLOCK / 64) * NS * P * 3u * sizeof(double)) + wv * NS * P;
         constexpr uint32_t NO_GROUP = 0xFFFFFFFFu, PAD_XY = 0xFFFFFFFFu;
-        uint32_t gid0 = NO_GROUP, gid1 = NO_GROUP;  // group held by each slot (wave-uniform)
-        uint32_t done0 = 0, done1 = 0;              // finished samples per slot
+        uint32_t gids[NS], dones[NS];  // group held by each slot and its finished samples (wave-uniform)
+#pragma unroll
+        for (uint32_t k = 0; k < NS; ++k) {
+            gids[k] = NO_GROUP;
+            dones[k] = 0;
+        }
         uint32_t cs = 0, next = GS;                 // claiming from slot cs at index next
-        bool ready = false;                         // slot cs ^ 1 holds a group not yet claimed from
+        bool ready = false;                         // slot (cs + 1) % NS holds a group not yet claimed from
         bool exhausted = false;                     // the queue is empty
         // Per-XCD queue heads: head x hands out the x-th contiguous eighth of the groups,
         // and a wave pulls from its own XCD's head first (then the next heads in turn), so
@@ -1726,7 +1824,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
         uint32_t qk = 0;  // heads found empty so far (wave-uniform)
-        auto fetch = [&]() {                        // uniform: take the next group into slot cs ^ 1
+        auto fetch = [&](uint32_t r) {              // uniform: take the next group into (free) slot r
             uint32_t gid = 0xFFFFFFFFu;
             if (lane == 0) {
                 for (; qk < QUEUE_HEADS; ++qk) {
@@ -1746,7 +1844,6 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             qk = __builtin_amdgcn_readlane(qk, 0);
             exhausted = gid == 0xFFFFFFFFu;  // (plain stores and selects: the flags stay in registers)
             if (exhausted) return;
-            const uint32_t r = cs ^ 1u;
             const uint32_t base = p.pixel_begin + gid * P;
             double* a = acc + r * P * 3u;
             uint32_t* xy = slot_xy + r * P;
@@ -1758,10 +1855,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            gid0 = r ? gid0 : gid;
-            gid1 = r ? gid : gid1;
-            done0 = r ? done0 : 0u;
-            done1 = r ? 0u : done1;
+#pragma unroll
+            for (uint32_t k = 0; k < NS; ++k) {
+                gids[k] = k == r ? gid : gids[k];
+                dones[k] = k == r ? 0u : dones[k];
+            }
             ready = true;
         };
         auto flush = [&](uint32_t gid, uint32_t r) {  // uniform: the group's last sample has finished
@@ -1819,15 +1917,22 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             // Group bookkeeping at the loop head, where little state is live: write out
             // finished groups, and take the next group into the free slot as soon as
             // fewer than a wave's worth of samples are left to claim.
-            if (gid0 != NO_GROUP && done0 == GS) {
-                flush(gid0, 0u);
-                gid0 = NO_GROUP;
+#pragma unroll
+            for (uint32_t k = 0; k < NS; ++k) {
+                if (gids[k] != NO_GROUP && dones[k] == GS) {
+                    flush(gids[k], k);
+                    gids[k] = NO_GROUP;
+                }
             }
-            if (gid1 != NO_GROUP && done1 == GS) {
-                flush(gid1, 1u);
-                gid1 = NO_GROUP;
+            if constexpr (NS == 2) {
+                if (!exhausted && !ready && GS - next < 64u && (cs ? gids[0] : gids[1]) == NO_GROUP) fetch(cs ^ 1u);
+            } else if (!exhausted && !ready && GS - next < 64u) {
+                const uint32_t r = (cs + 1u) & (NS - 1u);
+                bool free = false;
+#pragma unroll
+                for (uint32_t k = 0; k < NS; ++k) free |= k == r && gids[k] == NO_GROUP;
+                if (free) fetch(r);
             }
-            if (!exhausted && !ready && GS - next < 64u && (cs ? gid0 : gid1) == NO_GROUP) fetch();
             if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
             const unsigned long long t0 = stamp();
             HitMin<R, MAXD> hm;
@@ -1841,9 +1946,12 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = alive && ts.busy();
                     if (__ballot(going) == 0ull) break;
                     if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack);
+                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
                 }
                 sh = alive && !ts.busy();
+                if constexpr (PROF) {
+                    if (sh) prof_event(prof[wave], PROF_ROUNDS, PROF_ROUND_LANES);
+                }
                 traced = sh && !killed && b < p.max_bounces;
                 hm.t = ts.t_best;
                 hm.prim = (uint32_t)ts.best;
@@ -1871,11 +1979,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 atomicAdd(a + 1, rint((double)contrib.y * p.acc_scale));
                 atomicAdd(a + 2, rint((double)contrib.z * p.acc_scale));
             }
-            done0 += (uint32_t)__popcll(__ballot(ends && slot == 0u));
-            done1 += (uint32_t)__popcll(__ballot(ends && slot == 1u));
+#pragma unroll
+            for (uint32_t k = 0; k < NS; ++k) dones[k] += (uint32_t)__popcll(__ballot(ends && slot == k));
 
             // lanes without a path claim the next samples, in lane order: slot cs from
-            // `next`, then the group waiting in slot cs ^ 1
+            // `next`, then the group waiting in slot (cs + 1) % NS
             const bool want = ends || !alive;
             const uint64_t em = __ballot(want);
             const uint32_t nwant = (uint32_t)__popcll(em);
@@ -1885,7 +1993,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const uint32_t cs0 = cs;
             next += granted;
             if (next >= GS && ready) {
-                cs ^= 1u;
+                cs = NS == 2 ? cs ^ 1u : (cs + 1u) & (NS - 1u);
                 next -= GS;
                 ready = false;
             }
@@ -1893,7 +2001,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 alive = rank < granted;
                 if (alive) {
                     const bool second = claim >= GS;
-                    slot = second ? cs0 ^ 1u : cs0;
+                    slot = second ? (NS == 2 ? cs0 ^ 1u : (cs0 + 1u) & (NS - 1u)) : cs0;
                     const uint32_t idx = second ? claim - GS : claim;
                     j = idx & (P - 1u);
                     cur = idx >> logP;

@@ -38,7 +38,7 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
         hipLaunchKernelGGL(kernel, dim3((npix + dev::BLOCK - 1) / dev::BLOCK), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
     } else {
         RenderParams p = p0;
-        auto ring_bytes = [](uint32_t wp) { return (dev::BLOCK / 64) * 2u * wp * (3u * (uint32_t)sizeof(double) + 4u); };
+        auto ring_bytes = [](uint32_t wp) { return dev::philox_pool_bytes<MAXD>(wp); };
         uint32_t wp = p.wave_pixels;
         if (!wp) {
             wp = 1;

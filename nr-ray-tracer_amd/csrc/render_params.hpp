@@ -44,6 +44,10 @@ struct RenderParams {
     float* out;  // rows * width * 3 floats, row-major (Rgb32FImage layout)
     // Optional per-launch work counters (nullptr = off): see render.hip.
     unsigned long long* counters;
+    // Exact kernel, small scenes: test every primitive of the reference tree in its depth-first
+    // order instead of culling with the boxes (every lane walks the same node sequence, so the
+    // traversal does not diverge; the closest hit and its tie-break are the reference's).
+    uint32_t exact_all;
 };
 
 }  // namespace nrt

@@ -363,9 +363,10 @@ class Scene:
         """Diagnostic render with per-wave stamps: cycle shares of camera / trace / shading."""
         cam = camera or self.camera
         o = _opts(precision, rng, device, 0, 1, trace)
-        out = (C.c_uint64 * 8)()
-        _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 8))
-        iters, cam_c, trace_c, shade_c, waves, rec_c, rng_c, scat_c = list(out)
+        out = (C.c_uint64 * 16)()
+        _check(lib().nrt_debug_phase_profile(self._h, C.byref(cam._c()), C.byref(o), out, 16))
+        iters, cam_c, trace_c, shade_c, waves, rec_c, rng_c, scat_c = list(out)[:8]
+        vt, vl, lt, ll, rt, rl = list(out)[8:14]
         res = {"iterations_per_wave": iters / max(waves, 1), "waves": waves}
         if rng == "philox":
             # sample-pool loop: camera rays are part of the shading step; slot 1 counts
@@ -379,6 +380,11 @@ class Scene:
         res.update({"trace_share": trace_c / tot, "shade_share": shade_c / tot,
                     "shade_record_share": rec_c / tot, "shade_rng_share": rng_c / tot,
                     "shade_scatter_share": scat_c / tot, "cycles_per_iteration": tot / max(iters, 1)})
+        if vt:  # world-BVH traversal events (wave trips and active lanes per trip)
+            res.update({"visit_trips_per_wave": vt / max(waves, 1), "visit_lane_util": vl / (64.0 * vt),
+                        "leaf_trips_per_wave": lt / max(waves, 1), "leaf_lane_util": ll / (64.0 * max(lt, 1)),
+                        "shade_rounds_per_wave": rt / max(waves, 1), "shade_round_lane_util": rl / (64.0 * max(rt, 1)),
+                        "node_visits": vl, "prim_tests": ll, "rays_shaded": rl})
         return res
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",

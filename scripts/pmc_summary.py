@@ -55,6 +55,16 @@ def main():
         clk = per["GRBM_GUI_ACTIVE"] / 8.0
         out["clock_mhz"] = clk / (out["avg_ns"] * 1e-9) / 1e6 if out.get("avg_ns") else None
         out["valu_issue_frac"] = per["SQ_INSTS_VALU"] * 2.0 / (1024.0 * clk)
+    if "SQ_WAIT_INST_ANY" in per and per.get("SQ_WAVE_CYCLES"):
+        out["wait_inst_frac"] = per["SQ_WAIT_INST_ANY"] / per["SQ_WAVE_CYCLES"]
+        out["wait_any_frac"] = per.get("SQ_WAIT_ANY", 0.0) / per["SQ_WAVE_CYCLES"]
+    if per.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_bank_conflict_frac"] = per.get("SQ_LDS_BANK_CONFLICT", 0.0) / per["SQ_LDS_IDX_ACTIVE"]
+    if per.get("TCC_HIT_sum", 0.0) + per.get("TCC_MISS_sum", 0.0) > 0:
+        out["tcc_hit_rate"] = per["TCC_HIT_sum"] / (per["TCC_HIT_sum"] + per["TCC_MISS_sum"])
+    if per.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+        # vector L1 requests that went on to L2 per L1 access (1 - L1 hit rate, approximately)
+        out["tcp_to_tcc_frac"] = per.get("TCP_TCC_READ_REQ_sum", 0.0) / per["TCP_TOTAL_CACHE_ACCESSES_sum"]
     text = json.dumps(out, indent=1, sort_keys=True)
     print(text)
     if a.json:

@@ -1,5 +1,6 @@
 # usage: bash scripts/profile.sh <tag> <bench args...>
-# kernel-trace + stats summary, then PMC passes (one counter group per pass, no trace domains)
+# kernel-trace + stats summary, then PMC passes (one counter group per pass, no trace domains,
+# each pass within the per-block slot limits: SQ 8, TCC 4, TCP 4, GRBM 2)
 set -o pipefail
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
@@ -7,11 +8,11 @@ out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $out/bench_trace.json 2> $out/bench_trace.err || { echo "trace run failed"; tail -5 $out/bench_trace.err; exit 1; }
 i=0
-for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INSTS_SMEM" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
-           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_FLAT SQ_INST_CYCLES_VMEM_RD" \
-           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $pmc -d $out/pmc$i -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > $out/bench_pmc$i.json 2> $out/bench_pmc$i.err || { echo "pmc pass $i ($pmc) failed"; tail -3 $out/bench_pmc$i.err; }
+  timeout -s KILL 120 rocprofv3 --pmc $pmc -d $out/pmc$i -o run --output-format csv -- python3 bench.py --no-cpu-baseline --kernel-only --steps 2 --warmup 1 "$@" > $out/bench_pmc$i.json 2> $out/bench_pmc$i.err || { echo "pmc pass $i ($pmc) failed"; tail -3 $out/bench_pmc$i.err; }
 done
 echo "profile $tag done"

@@ -1,13 +1,16 @@
-"""Copy one round-profile run (scripts/round_profile.sh <tag>) from gpurun_out/ into profiles/.
+"""Copy profile runs (scripts/profile.sh <tag>_<variant> ...) from gpurun_out/ into profiles/.
 
-usage: python scripts/publish_profiles.py <tag> [--as r01]
+usage: python scripts/publish_profiles.py <tag> [--as r02] [--bench <tag>_bench_default.json]
 
-Writes profiles/<as>_<variant>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
-profiles/<as>_<variant>_pmc.json (scripts/pmc_summary.py over the PMC passes),
-profiles/<as>_bench_default.json (the default bench line of the same call) and
-profiles/pmc_summary.json, the per-variant figures bench.py quotes in its roofline block.
+For every gpurun_out/prof_<tag>_<variant>/ directory writes
+  profiles/<as>_<variant>_kernel_stats.csv  (rocprofv3 --kernel-trace --stats summary)
+  profiles/<as>_<variant>_pmc.json          (scripts/pmc_summary.py over the PMC passes)
+and profiles/pmc_summary.json: one entry per variant, keyed by the exact bench configuration
+of that run (scene, width, height, spp, precision, rng, trace, n_gpus, read from the bench line
+the kernel-trace run printed), which bench.py looks up for its roofline block.
 """
 import argparse
+import glob
 import json
 import os
 import shutil
@@ -15,38 +18,50 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = ("f32_philox", "f64_chacha8")
+KEY = ("scene", "width", "height", "spp", "precision", "rng", "trace")
+KEEP = ("kernel", "avg_ns", "calls", "hbm_bytes_per_launch", "hbm_fetch_bytes", "hbm_write_bytes",
+        "valu_lane_utilization", "valu_insts_per_wave", "valu_issue_frac", "clock_mhz", "wait_inst_frac",
+        "wait_any_frac", "lds_bank_conflict_frac", "tcc_hit_rate", "tcp_to_tcc_frac")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--as", dest="name", default="r01")
+    ap.add_argument("--as", dest="name", default="r02")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
-    summary = {}
-    for v in VARIANTS:
-        src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}_{v}")
-        if not os.path.isdir(src):
-            sys.exit(f"missing {src}")
-        shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
-                    os.path.join(prof, f"{a.name}_{v}_kernel_stats.csv"))
+    entries = []
+    dirs = sorted(glob.glob(os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}_*")))
+    if not dirs:
+        sys.exit(f"no gpurun_out/prof_{a.tag}_* directories")
+    for src in dirs:
+        v = os.path.basename(src)[len(f"prof_{a.tag}_"):]
+        stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+        if not os.path.exists(stats):
+            stats = next(iter(glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)), None)
+        if stats is None:
+            print(f"skip {v}: no kernel stats")
+            continue
+        shutil.copy(stats, os.path.join(prof, f"{a.name}_{v}_kernel_stats.csv"))
         pmc_json = os.path.join(prof, f"{a.name}_{v}_pmc.json")
         subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), src, "--json", pmc_json],
                        check=True, capture_output=True)
         with open(pmc_json) as fh:
             d = json.load(fh)
-        keep = ("kernel", "avg_ns", "hbm_bytes_per_launch", "hbm_fetch_bytes", "hbm_write_bytes",
-                "valu_lane_utilization", "valu_insts_per_wave", "valu_issue_frac", "clock_mhz")
-        summary[v] = {k: d.get(k) for k in keep}
-        summary[v]["source"] = (f"profiles/{a.name}_{v}_pmc.json (rocprofv3 --pmc, one counter group per pass; "
-                                f"FETCH_SIZE x2 per MI355X_MICROARCH.md; valu_issue_frac in 2-cycle wave64 slots)")
-    bench = os.path.join(ROOT, "gpurun_out", f"{a.tag}_bench_default.json")
-    if os.path.exists(bench):
-        shutil.copy(bench, os.path.join(prof, f"{a.name}_bench_default.json"))
+        with open(os.path.join(src, "bench_trace.json")) as fh:
+            bench = json.loads(fh.read().strip().splitlines()[-1])
+        e = {k: bench["config"][k] for k in KEY}
+        e["n_gpus"] = bench["n_gpus"]
+        e["variant"] = v
+        e.update({k: d.get(k) for k in KEEP})
+        e["bench_kernel_ms"] = bench["roofline"]["kernel_ms"]
+        e["source"] = (f"profiles/{a.name}_{v}_pmc.json + {a.name}_{v}_kernel_stats.csv (rocprofv3 --kernel-trace "
+                       f"--stats, then --pmc, one counter group per pass; FETCH_SIZE x2 per MI355X_MICROARCH.md; "
+                       f"valu_issue_frac in 2-cycle wave64 slots)")
+        entries.append(e)
     with open(os.path.join(prof, "pmc_summary.json"), "w") as fh:
-        fh.write(json.dumps(summary, indent=1) + "\n")
-    print(json.dumps(summary, indent=1))
+        fh.write(json.dumps({"round": a.name, "entries": entries}, indent=1) + "\n")
+    print(json.dumps(entries, indent=1))
 
 
 if __name__ == "__main__":
