@@ -353,7 +353,7 @@ def main():
                         "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
                         "traffic": traffic},
                 "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
-                                                "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
+                                                "valu_busy_est", "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
                                                 "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
                 "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
                         "divergence; its HBM traffic is the framebuffer plus a few KB of scene"},

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 2
+#define NRT_ABI_VERSION 3
 
 enum {
     NRT_OK = 0,
@@ -130,7 +130,14 @@ typedef struct {
     uint32_t coplanar_pairs; /* overlapping coplanar surface pairs (their hits tie in the reference) */
     uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
                                 (else AUTO takes the world BVH, which compares tie keys) */
+    uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
+    uint32_t reserved;
 } nrt_scene_stats;
+/* Exact-kernel traversal (same closest hit and tie-break as BVH::hit, object.rs:89-121):
+ *   BVH      the reference tree, box by box
+ *   ALL      every primitive in the tree's depth-first order, no boxes (at most 48 primitives)
+ *   WORLD    the f32 world BVH culls (conservatively), the reference tests decide */
+enum nrt_exact_mode { NRT_EXACT_BVH = 0, NRT_EXACT_ALL = 1, NRT_EXACT_WORLD = 2 };
 
 typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);
 

@@ -181,6 +181,14 @@ static uint64_t exact_walk_prims(const FlatScene& f, int32_t node, uint64_t cap,
 }
 constexpr uint64_t EXACT_ALL_MAX = 48;  // Cornell box: 18 quads (6 walls + two 6-quad cubes)
 
+// nrt_exact_mode of a scene (RenderParams::exact_all / exact_wbvh; NRT_EXACT_ALL / NRT_EXACT_WBVH
+// environment knobs override it for A/B runs).
+static uint32_t exact_mode(const FlatScene& f) {
+    if (exact_walk_prims(f, f.root, EXACT_ALL_MAX) <= EXACT_ALL_MAX) return NRT_EXACT_ALL;
+    if (!f.wexact.empty()) return NRT_EXACT_WORLD;
+    return NRT_EXACT_BVH;
+}
+
 RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t rows, const FlatScene& f) {
     if (c.width == 0 || c.height == 0) throw std::invalid_argument("image width and height must be > 0");
     if (c.width * c.height > 0xFFFFFFFFull) throw std::invalid_argument("image has more than 2^32 pixels");
@@ -205,8 +213,11 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) p.wave_wait = (uint32_t)v;
     }
-    p.exact_all = exact_walk_prims(f, f.root, EXACT_ALL_MAX) <= EXACT_ALL_MAX ? 1u : 0u;
+    const uint32_t mode = exact_mode(f);
+    p.exact_all = mode == NRT_EXACT_ALL ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_ALL")) p.exact_all = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+    p.exact_wbvh = (!p.exact_all && mode == NRT_EXACT_WORLD) ? 1u : 0u;
+    if (const char* e = std::getenv("NRT_EXACT_WBVH")) p.exact_wbvh = std::strtol(e, nullptr, 10) != 0 && !f.wexact.empty();
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;
@@ -523,6 +534,8 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
         out->world_prims = f.world_ok ? f.world_units : 0;
         out->coplanar_pairs = f.coplanar_pairs;
         out->world_list_ok = f.world_ok && f.list_ok ? 1u : 0u;
+        out->exact_mode = exact_mode(f);
+        out->reserved = 0;
         return NRT_OK;
     });
 }

@@ -178,8 +178,19 @@ struct alignas(16) DBvh4Node {
 static_assert(sizeof(DBvh4Node) == 64, "one half cache line per 4-wide node");
 constexpr int32_t WBVH_DONE = INT32_MIN;  // "stack empty" marker (never a valid leaf ref)
 constexpr int32_t WBVH_NO_LEAF = 0;       // "no parked leaf" (leaf refs are negative)
-constexpr uint32_t WBVH_STACK = 32;       // per-lane stack entries (host checks the tree depth)
+constexpr uint32_t WBVH_STACK = 32;       // per-lane stack entries at most (host checks the tree's bound)
 constexpr uint32_t WBVH_LEAF_MAX = 8;
+
+// Exact kernel over the world BVH (RenderParams::exact_wbvh): for each BVH primitive slot,
+// the reference primitive it is (DPrim index), the instance whose Translate/Rotate/Scale
+// chain maps the world ray into that primitive's object space (-1: none), and its rank in the
+// reference's depth-first candidate order (ties go to the higher rank, object.rs:109-115).
+struct alignas(16) DExactRef {
+    uint32_t prim;
+    int32_t inst;
+    uint32_t rank;
+    uint32_t pad;
+};
 
 template <typename Real>
 struct alignas(16) DXform {
@@ -263,6 +274,11 @@ struct DSceneView {
     int32_t wbvh4_root;
     int32_t wbvh_root;               // child ref of the root
     uint32_t n_wbvh;
+    // per-lane stack entries the tree in use can need (<= WBVH_STACK): the world-BVH kernels
+    // allocate that many + 1 (branch-free pushes) in LDS, so shallow trees leave room for
+    // more workgroups per CU
+    uint32_t wbvh_stack;
+    const DExactRef* wexact;  // f64 view: exact reference of each world-BVH slot (exact_wbvh mode)
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each

@@ -3,6 +3,7 @@
 
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <algorithm>
@@ -835,7 +836,14 @@ struct Flattener {
     // the kernel's stack) leave wbvh_ok false and the instance BVH in charge.
     void build_wbvh() {
         std::vector<std::array<double, 6>> bounds(out.wprims.size());
-        std::vector<float> cost(out.wprims.size(), 1.0f);  // f64 sphere tests cost ~4 plane tests
+        // SAH weights relative to a (binary) node visit: a plane test; f64 sphere tests cost ~4 of
+        // them.  Tuning knob NRT_SAH_PRIM_COST scales the plane-test weight (host build only).
+        float prim_cost = 1.0f;
+        if (const char* e = std::getenv("NRT_SAH_PRIM_COST")) {
+            const float v = std::strtof(e, nullptr);
+            if (v > 0.0f && v < 100.0f) prim_cost = v;
+        }
+        std::vector<float> cost(out.wprims.size(), prim_cost);
         for (size_t i = 0; i < out.wprims.size(); ++i) {
             const DPrimWorld<double>& w = out.wprims[i];
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -844,7 +852,7 @@ struct Flattener {
             };
             const uint32_t kind = w.meta & WKIND_MASK;
             if (kind == PRIM_SPHERE) {  // center(t) = N + t * speed, t in [0, 1]
-                cost[i] = NRT_SPHERE_COST;
+                cost[i] = NRT_SPHERE_COST * prim_cost;
                 for (int end = 0; end < 2; ++end)
                     for (int sg = -1; sg <= 1; sg += 2) {
                         double p[3];
@@ -1044,9 +1052,56 @@ float round_up(double x) {
 
 }  // namespace
 
+// World primitive k (the reference's depth-first candidate order, world_walk) is the k-th
+// primitive of a full depth-first walk of the exact tree (every box taken); record the DPrim
+// and instance of each BVH slot for the exact kernel's world-BVH mode.  Nested instances, or
+// any disagreement in count or kind, leave the mapping empty (mode unavailable).
+static void map_exact_refs(FlatScene& s) {
+    s.wexact.clear();
+    if (!s.wbvh_ok || s.wbvh.order.empty()) return;
+    std::vector<std::pair<uint32_t, int32_t>> seq;
+    bool ok = true;
+    auto walk = [&](int32_t node, int32_t inst, auto&& self) -> void {
+        while (ok && node >= 0 && node < (int32_t)s.nodes.size()) {
+            const DNode<double>& d = s.nodes[node];
+            const uint32_t kind = d.meta & 3u;
+            if (kind == NODE_INNER) {
+                ++node;
+                continue;
+            }
+            if (kind == NODE_PRIM) {
+                seq.emplace_back(d.meta >> 2, inst);
+            } else if (kind == NODE_INSTANCE) {
+                const uint32_t idx = d.meta >> 2;
+                if (inst >= 0 || idx >= s.instances.size()) {
+                    ok = false;
+                    return;
+                }
+                self(s.instances[idx].root, (int32_t)idx, self);
+            } else {
+                ok = false;
+                return;
+            }
+            node = d.skip;
+        }
+    };
+    walk(s.root, -1, walk);
+    if (!ok || seq.size() != s.wbvh.order.size()) return;
+    std::vector<DExactRef> refs(s.wbvh.order.size());
+    for (size_t slot = 0; slot < refs.size(); ++slot) {
+        const uint32_t rank = s.wbvh.order[slot];
+        if (rank >= seq.size()) return;
+        const auto& e = seq[rank];
+        if (e.first >= s.prims.size() || s.prims[e.first].kind != (s.wbvh_prims[slot].meta & WKIND_MASK)) return;
+        refs[slot] = DExactRef{e.first, e.second, rank, 0u};
+    }
+    s.wexact = std::move(refs);
+}
+
 FlatScene flatten_scene(const ObjectPtr& top) {
     Flattener f;
     f.run(top.get());
+    map_exact_refs(f.out);
     return std::move(f.out);
 }
 

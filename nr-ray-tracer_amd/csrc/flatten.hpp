@@ -39,6 +39,9 @@ struct FlatScene {
     WorldBvh wbvh;
     std::vector<DPrimWorld<double>> wbvh_prims;  // BVH leaf order
     bool wbvh_ok = false;
+    // Exact reference of each BVH slot (device_scene.hpp DExactRef), when every world
+    // primitive maps onto the exact tree's depth-first walk (instances not nested).
+    std::vector<DExactRef> wexact;
 };
 
 FlatScene flatten_scene(const ObjectPtr& top_level_bvh);

@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "device_scene.hpp"
@@ -30,6 +31,12 @@ namespace dev {
 constexpr int BLOCK = 256;
 #ifndef NRT_SPECULATIVE
 #define NRT_SPECULATIVE 1  // world-BVH rounds: lanes holding a leaf keep descending (Aila & Laine)
+#endif
+#ifndef NRT_CAM_RELOAD
+#define NRT_CAM_RELOAD 0
+#endif
+#ifndef NRT_WBVH_SORT
+#define NRT_WBVH_SORT 0  // 4-wide visits: 1 = full sorting network; 0 = nearest hit child first, the rest in slot order (C4 +4 %)
 #endif
 #ifndef NRT_WBVH_IFIF
 #define NRT_WBVH_IFIF 0  // world BVH: one node visit or one primitive per lane and trip (wbvh_trip)
@@ -812,10 +819,16 @@ struct WbvhTrav {
     __device__ __forceinline__ bool busy() const { return node != WBVH_DONE || leaf != WBVH_NO_LEAF; }
 };
 
+// 1/d clamped to +-1e20 (d = +-0 would give +-inf, and inf * 0 = NaN in the 4-wide node
+// decode): a ray parallel to a slab then gets huge finite slab ends of the right signs.
+__device__ __forceinline__ float wbvh_inv(float d) {
+    const float r = __builtin_amdgcn_rcpf(d);
+    return __builtin_copysignf(fminf(fabsf(r), 1e20f), r);
+}
 __device__ __forceinline__ void wbvh_begin(WbvhTrav& ts, int32_t root, const Ray<float>& ray) {
-    ts.ix = __builtin_amdgcn_rcpf(ray.d.x);
-    ts.iy = __builtin_amdgcn_rcpf(ray.d.y);
-    ts.iz = __builtin_amdgcn_rcpf(ray.d.z);
+    ts.ix = wbvh_inv(ray.d.x);
+    ts.iy = wbvh_inv(ray.d.y);
+    ts.iz = wbvh_inv(ray.d.z);
     ts.ox = ray.o.x * ts.ix;
     ts.oy = ray.o.y * ts.iy;
     ts.oz = ray.o.z * ts.iz;
@@ -862,12 +875,15 @@ __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc,
     else wbvh_leaf_t<R, FLAT, false>(ts, sc, ray, ref, pc);
 }
 
+// Stacks: LDS, entry k of this lane at stack[k * BLOCK] (STRIDE = BLOCK), or a private
+// array (STRIDE = 1: the exact kernel's world-BVH mode, whose LDS holds the ChaCha8 ring).
+template <int STRIDE = BLOCK>
 __device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, const int32_t* stack) {
-    return ts.sp ? stack[(--ts.sp) * BLOCK] : WBVH_DONE;
+    return ts.sp ? stack[(--ts.sp) * STRIDE] : WBVH_DONE;
 }
 
 // Binary node visit: both child boxes, nearer hit child next, the other pushed.
-template <typename R>
+template <typename R, int STRIDE = BLOCK>
 __device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
     const DBvhNode nd = load16(sc.wbvh + t.node);
     const float a0x = nd.lo0[0] * t.ix - t.ox, b0x = nd.hi0[0] * t.ix - t.ox;
@@ -883,12 +899,12 @@ __device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc
     const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
     if (h0 && h1) {
         const bool near0 = tn0 <= tn1;
-        stack[(t.sp++) * BLOCK] = near0 ? nd.c1 : nd.c0;
+        stack[(t.sp++) * STRIDE] = near0 ? nd.c1 : nd.c0;
         t.node = near0 ? nd.c0 : nd.c1;
     } else if (h0 || h1) {
         t.node = h0 ? nd.c0 : nd.c1;
     } else {
-        t.node = wbvh_pop(t, stack);
+        t.node = wbvh_pop<STRIDE>(t, stack);
     }
 }
 
@@ -903,33 +919,52 @@ __device__ __forceinline__ void wbvh_cswap(float& ta, int32_t& ca, float& tb, in
     tb = sw ? t0 : tb;
     cb = sw ? c0 : cb;
 }
-template <typename R>
+template <typename R, int STRIDE = BLOCK>
 __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
     const DBvh4Node nd = load16(sc.wbvh4 + t.node);
     // plane t = (org + q * step - o) / d = q * (step / d) + (org / d - o / d)
     const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
     const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
     const float Az = __uint_as_float(((nd.exps >> 16) & 0xFFu) << 23) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
+    // The ray's direction signs pick each axis's near and far plane bytes for all four
+    // children at once (1/d is finite, wbvh_begin), so a child's slab needs no min/max, and an
+    // empty slot (qlo 255, qhi 0 on every axis) comes out with near > far: a miss.
+    const bool px = t.ix >= 0.0f, py = t.iy >= 0.0f, pz = t.iz >= 0.0f;
+    const uint32_t nqx = px ? nd.qlo[0] : nd.qhi[0], fqx = px ? nd.qhi[0] : nd.qlo[0];
+    const uint32_t nqy = py ? nd.qlo[1] : nd.qhi[1], fqy = py ? nd.qhi[1] : nd.qlo[1];
+    const uint32_t nqz = pz ? nd.qlo[2] : nd.qhi[2], fqz = pz ? nd.qhi[2] : nd.qlo[2];
     auto child_t = [&](int k) {  // entry distance of child k, +inf if missed or empty
         auto q = [&](uint32_t w) { return (float)((w >> (8 * k)) & 0xFFu); };
-        const float ax = q(nd.qlo[0]) * Ax + Bx, bx = q(nd.qhi[0]) * Ax + Bx;
-        const float ay = q(nd.qlo[1]) * Ay + By, by = q(nd.qhi[1]) * Ay + By;
-        const float az = q(nd.qlo[2]) * Az + Bz, bz = q(nd.qhi[2]) * Az + Bz;
-        const float n = fmaxf(fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz)), 0.0f);
-        const float f = fminf(fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)), t.t_best);
-        return ((n <= f) & (nd.child[k] != WBVH_DONE)) ? n : INFINITY;
+        const float nx = q(nqx) * Ax + Bx, fx = q(fqx) * Ax + Bx;
+        const float ny = q(nqy) * Ay + By, fy = q(fqy) * Ay + By;
+        const float nz = q(nqz) * Az + Bz, fz = q(fqz) * Az + Bz;
+        const float n = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.0f));
+        const float f = fminf(fminf(fx, fy), fminf(fz, t.t_best));
+        return n <= f ? n : INFINITY;
     };
     float t0 = child_t(0), t1 = child_t(1), t2 = child_t(2), t3 = child_t(3);
     int32_t c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+#if NRT_WBVH_SORT
     wbvh_cswap(t0, c0, t1, c1);
     wbvh_cswap(t2, c2, t3, c3);
     wbvh_cswap(t0, c0, t2, c2);
     wbvh_cswap(t1, c1, t3, c3);
     wbvh_cswap(t1, c1, t2, c2);
-    if (t3 != INFINITY) stack[(t.sp++) * BLOCK] = c3;
-    if (t2 != INFINITY) stack[(t.sp++) * BLOCK] = c2;
-    if (t1 != INFINITY) stack[(t.sp++) * BLOCK] = c1;
-    t.node = t0 != INFINITY ? c0 : wbvh_pop(t, stack);
+#else
+    // nearest hit child first; the others keep their slots (pushed 3, 2, 1: child order)
+    wbvh_cswap(t0, c0, t1, c1);
+    wbvh_cswap(t0, c0, t2, c2);
+    wbvh_cswap(t0, c0, t3, c3);
+#endif
+    // branch-free pushes: every slot is written at sp, sp advances past the hit ones (the
+    // stack has one spare entry above the tree's bound for the writes that do not count)
+    stack[t.sp * STRIDE] = c3;
+    t.sp += t3 != INFINITY ? 1u : 0u;
+    stack[t.sp * STRIDE] = c2;
+    t.sp += t2 != INFINITY ? 1u : 0u;
+    stack[t.sp * STRIDE] = c1;
+    t.sp += t1 != INFINITY ? 1u : 0u;
+    t.node = t0 != INFINITY ? c0 : wbvh_pop<STRIDE>(t, stack);
 }
 
 // One round: descend through inner nodes until the lane holds a leaf (or is
@@ -1157,12 +1192,77 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
     return found;
 }
 
+// Exact kernel, world-BVH mode (RenderParams::exact_wbvh; large scenes whose instances do
+// not nest, e.g. the teapot): the f32 world BVH (binned SAH, 4-wide) only culls, and every
+// primitive in a reached leaf gets the reference's own test in f64 in its object space
+// (xform_in, then Sphere::hit / Plane::hit, sphere.rs:105-163, plane.rs:141-174).  The winner
+// is the smallest exact t, ties to the higher depth-first rank (object.rs:109-115), so the
+// visiting order does not matter.  The culling is conservative: the f32 boxes are rounded
+// outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
+// inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
+// private array (the LDS holds the ChaCha8 ring).
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
+    Ray<float> fr;
+    fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    WbvhTrav ts;
+    wbvh_begin(ts, wbvh_root(sc), fr);
+    int32_t stk[WBVH_STACK + 1];
+    R best_t = R(INFINITY);
+    uint32_t best_rank = 0;
+    int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
+    Ray<R> oray = wray;
+    while (true) {
+        while (ts.node >= 0) {
+            if (sc.wbvh4) wbvh4_visit<R, 1>(ts, sc, stk);
+            else wbvh2_visit<R, 1>(ts, sc, stk);
+        }
+        if (ts.node == WBVH_DONE) break;
+        const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const DExactRef ref = sc.wexact[first + k];
+            if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
+                oray = wray;
+                if (ref.inst >= 0) xform_in<R, true>(sc, sc.instances[ref.inst], oray);
+                cur_inst = ref.inst;
+            }
+            const DPrim<R>& pr = sc.prims[ref.prim];
+            R t;
+            if (pr.kind == PRIM_SPHERE) {
+                t = sphere_t(pr, oray);
+            } else {
+                R alpha, beta;
+                V<R> point;
+                t = plane_t(pr, oray, alpha, beta, point);
+            }
+            if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
+                best_t = t;
+                best_rank = ref.rank;
+                best_prim = (int32_t)ref.prim;
+                best_inst = ref.inst;
+                ts.t_best = (float)best_t * (1.0f + 0x1p-20f);
+            }
+        }
+        ts.node = wbvh_pop<1>(ts, stk);
+    }
+    hm.t = best_t;
+    hm.prim = (uint32_t)best_prim;
+    hm.depth = best_inst >= 0 ? 1 : 0;
+    hm.inst[0] = (uint32_t)best_inst;
+    return best_prim >= 0;
+}
+
 template <typename R, int MAXD, bool EXACT, bool FLAT = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                      int32_t* stack, bool all = false) {
+                                      int32_t* stack, bool all = false, bool exact_wbvh = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
-    else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
+    else if constexpr (EXACT && sizeof(R) == 8) {
+        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+        return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
+    } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
 
 // HitRecord of the winner (HitRecord::new_with_uv, hitable.rs:38-59).
@@ -1496,6 +1596,10 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #define NRT_F64_WAVES 4  // f64 kernels: 4 waves per SIMD (C5 410 -> 274 ms, C4 248 -> 158 ms; 3, 5, 6 slower)
 #endif
     if (sizeof(R) == 8) return NRT_F64_WAVES;
+#ifndef NRT_WBVH_WAVES
+#define NRT_WBVH_WAVES 1
+#endif
+    if (sizeof(R) == 4 && MAXD < 0 && !G::uses_lds) return NRT_WBVH_WAVES;
     if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT)) return NRT_FLAT_WAVES;
     return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
 }
@@ -1549,16 +1653,31 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
-    constexpr uint32_t stack_bytes = MAXD < 0 ? WBVH_STACK * BLOCK * sizeof(int32_t) : 0;
+    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t) : 0u;
     int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
 
     G g;
-    const V<R> top_left = cam3<R>(p, 0, p.top_left), du = cam3<R>(p, 1, p.pixel_delta_u);
-    const V<R> dv = cam3<R>(p, 2, p.pixel_delta_v), look_from = cam3<R>(p, 3, p.look_from);
-    const V<R> disk_u = cam3<R>(p, 4, p.defocus_disk_u), disk_v = cam3<R>(p, 5, p.defocus_disk_v);
-    const V<R> background = cam3<R>(p, 6, p.background);
+    // Camera vectors (camera.rs:205-227) q = 0..6: top_left, delta_u, delta_v, look_from,
+    // disk_u, disk_v, background.  f32 (NRT_CAM_RELOAD): read from the kernel arguments where
+    // used, through a pointer the compiler cannot see through, so the 21 floats do not hold
+    // SGPRs across the loop (the loop is at the SGPR limit and spills into VGPR lanes).
+    auto cam = [&](int q) -> V<R> {
+        if constexpr (sizeof(R) == 4 && NRT_CAM_RELOAD) {
+            // the kernel's first argument is `p`: its camf member sits at a fixed kernarg offset
+            using KF = const __attribute__((address_space(4))) float*;
+            KF c = (KF)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                        offsetof(RenderParams, camf));
+            asm volatile("" : "+s"(c));
+            return mk(c[3 * q], c[3 * q + 1], c[3 * q + 2]);
+        } else {
+            const double* d = q == 0 ? p.top_left : q == 1 ? p.pixel_delta_u : q == 2 ? p.pixel_delta_v
+                            : q == 3 ? p.look_from : q == 4 ? p.defocus_disk_u : q == 5 ? p.defocus_disk_v
+                            : p.background;
+            return cam3<R>(p, q, d);
+        }
+    };
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform values live in SGPRs
 
     uint32_t b = 0;  // bounces of this path
@@ -1600,7 +1719,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         contrib = mk(R(0), R(0), R(0));
         if (!traced) return false;
         if (!hit) {
-            contrib = tp * background;
+            contrib = tp * cam(6);  // background
             return false;
         }
         h = make_record<R, MAXD, EXACT, FLAT>(sc, ray, hm);
@@ -1676,9 +1795,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ox = draw<R>(g, R(-0.5), R(0.5));
                 oy = draw<R>(g, R(-0.5), R(0.5));
             }
-            const V<R> point = (top_left + ((R)x + ox) * du) + ((R)y + oy) * dv;
+            const V<R> point = (cam(0) + ((R)x + ox) * cam(1)) + ((R)y + oy) * cam(2);
             const V<R> disk = random_in_unit_disk<R>(g);
-            ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+            ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
             prep_ray<R, EXACT>(ray);
@@ -1768,7 +1887,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
-                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0);
+                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0,
+                                                      p.exact_wbvh != 0);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);
@@ -1890,13 +2010,13 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ox = u01<R>(w.x) - R(0.5);
                 oy = u01<R>(w.y) - R(0.5);
             }
-            const V<R> point = (top_left + ((R)px + ox) * du) + ((R)py + oy) * dv;
+            const V<R> point = (cam(0) + ((R)px + ox) * cam(1)) + ((R)py + oy) * cam(2);
             if (p.defocus) {
                 const uint4 wd = g.block_at(pixel_index(), cur, PHILOX_STEP_DEFOCUS);
                 const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
-                ray.o = (look_from + disk.x * disk_u) + disk.y * disk_v;
+                ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
             } else {
-                ray.o = look_from;  // zero disk: the draws would only scale zero vectors
+                ray.o = cam(3);  // zero disk: the draws would only scale zero vectors
             }
             ray.d = point - ray.o;
             ray.time = u01<R>(w.z);
@@ -1961,7 +2081,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 sh = alive;
                 traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
                 // world list: the global tables through the scalar cache; records read LDS
-                if (traced) hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack);
+                if (traced)
+                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0,
+                                                      p.exact_wbvh != 0);
             }
             const unsigned long long t1 = stamp();
             Rec<R> h;

@@ -68,7 +68,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
-                          (MAXD < 0 ? WBVH_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
+                          (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v);
     using dev::KF_FLAT;
     using dev::KF_PERLIN;

@@ -6,6 +6,7 @@
 
 #include "launch.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <stdexcept>
@@ -123,9 +124,15 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                        nt = (uint32_t)fs.textures.size();
         // f64 view: the exact node array (reference node for node); f32 view: the
         // list-collapsed array with composed instance transforms.
+        // the exact kernel's world-BVH mode culls with the f32 world BVH (same device arrays)
+        auto* wx = (DExactRef*)track(upload(fs.wexact, "wexact"), fs.wexact.size() * sizeof(DExactRef));
+        const bool wx_ok = !fs.wexact.empty();
+        const uint32_t wstack = std::max<uint32_t>(1u, use_wbvh4(fs) ? fs.wbvh.stack4 : fs.wbvh.depth);
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0, nullptr, 0, 0, nullptr, nullptr, WBVH_DONE, WBVH_DONE, 0};
+                                     nullptr, 0, nullptr, 0, 0, wx_ok ? wbn : nullptr,
+                                     (wx_ok && use_wbvh4(fs)) ? wb4 : nullptr, fs.wbvh.root4, fs.wbvh.root,
+                                     wx_ok ? (uint32_t)fs.wbvh.nodes.size() : 0u, wstack, wx_ok ? wx : nullptr};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
@@ -133,7 +140,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
                                     (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
                                     fs.wbvh.root4, fs.wbvh.root,
-                                    (uint32_t)fs.wbvh.nodes.size()};
+                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr};
         ds->wbvh_ok = fs.wbvh_ok;
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->flat = !ds->perlin;

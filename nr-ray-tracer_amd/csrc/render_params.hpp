@@ -48,6 +48,10 @@ struct RenderParams {
     // order instead of culling with the boxes (every lane walks the same node sequence, so the
     // traversal does not diverge; the closest hit and its tie-break are the reference's).
     uint32_t exact_all;
+    // Exact kernel, large scenes with a world BVH whose primitives map onto the exact tree
+    // (DSceneView::wexact): the f32 world BVH culls, the reference tests decide (kernel.hpp
+    // trace_exact_wbvh).
+    uint32_t exact_wbvh;
 };
 
 }  // namespace nrt

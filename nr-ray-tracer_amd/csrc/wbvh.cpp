@@ -266,6 +266,7 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
             }
             need[i] = (kids ? kids - 1 : 0) + deepest;
         }
+        bld.out.stack4 = need[bld.out.root4];
         if (need[bld.out.root4] > WBVH_STACK) {  // too deep for 4-wide traversal: binary only
             bld.out.nodes4.clear();
             bld.out.root4 = WBVH_DONE;

@@ -16,6 +16,7 @@ struct WorldBvh {
     uint32_t depth = 0;           // deepest inner-node level (stack bound)
     std::vector<DBvh4Node> nodes4;  // the same tree collapsed to 4-wide nodes
     int32_t root4 = WBVH_DONE;
+    uint32_t stack4 = 0;            // deepest per-lane stack the 4-wide traversal can reach
 };
 
 // bounds[i] = {lo.x, lo.y, lo.z, hi.x, hi.y, hi.z} of primitive i (world space, f64);

@@ -18,6 +18,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="render_kernel")
     ap.add_argument("--json")
+    ap.add_argument("--ubench", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "profiles", "r02_ubench_valu_cost.jsonl"),
+                    help="scripts/ubench/valu_cost output: per-class issue cost at 8 waves per SIMD")
     a = ap.parse_args()
     out = {}
     st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
@@ -65,6 +68,38 @@ def main():
     if per.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
         # vector L1 requests that went on to L2 per L1 access (1 - L1 hit rate, approximately)
         out["tcp_to_tcc_frac"] = per.get("TCP_TCC_READ_REQ_sum", 0.0) / per["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    # VALU busy estimate: each instruction class priced at its measured wall-clock issue cost per
+    # SIMD with 8 waves per SIMD on every CU (scripts/ubench/valu_cost.hip), over the SIMD cycles
+    # of the dispatch.  Unclassified VALU (compares, selects, moves, bit ops) at the v_add_f32 cost.
+    classes = {"SQ_INSTS_VALU_ADD_F32": "v_add_f32", "SQ_INSTS_VALU_MUL_F32": "v_mul_f32",
+               "SQ_INSTS_VALU_FMA_F32": "v_fma_f32", "SQ_INSTS_VALU_TRANS_F32": "v_exp_f32",
+               "SQ_INSTS_VALU_INT32": "v_xor_b32", "SQ_INSTS_VALU_INT64": "v_mad_u64_u32",
+               "SQ_INSTS_VALU_CVT": "v_cvt_f32_u32", "SQ_INSTS_VALU_FMA_F64": "v_fma_f64",
+               "SQ_INSTS_VALU_ADD_F64": "v_mul_f64", "SQ_INSTS_VALU_MUL_F64": "v_mul_f64",
+               "SQ_INSTS_VALU_TRANS_F64": "v_exp_f32"}
+    if os.path.exists(a.ubench) and out.get("clock_mhz") and "SQ_INSTS_VALU_FMA_F32" in per and "SQ_INSTS_VALU" in per:
+        cyc = {}
+        for line in open(a.ubench):
+            d = json.loads(line)
+            if d.get("waves_per_simd") == 8:
+                cyc[d["op"]] = d["clock_mhz"] * 1e6 / d["wall_wave_insts_per_s_per_simd"]
+        if all(v in cyc for v in classes.values()) and "v_add_f32" in cyc:
+            busy = 0.0
+            known = 0.0
+            mix = {}
+            for c, op in classes.items():
+                n = per.get(c, 0.0)
+                busy += n * cyc[op]
+                known += n
+                mix[c.replace("SQ_INSTS_VALU_", "")] = n / per["SQ_INSTS_VALU"]
+            other = max(per["SQ_INSTS_VALU"] - known, 0.0)
+            busy += other * cyc["v_add_f32"]
+            mix["OTHER"] = other / per["SQ_INSTS_VALU"]
+            simd_cycles = 1024.0 * out["clock_mhz"] * 1e6 * out["avg_ns"] * 1e-9
+            out["valu_mix"] = mix
+            out["valu_cycles_per_inst_est"] = busy / per["SQ_INSTS_VALU"]
+            out["valu_busy_est"] = busy / simd_cycles
+            out["valu_busy_source"] = a.ubench
     text = json.dumps(out, indent=1, sort_keys=True)
     print(text)
     if a.json:

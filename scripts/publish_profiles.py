@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEY = ("scene", "width", "height", "spp", "precision", "rng", "trace")
 KEEP = ("kernel", "avg_ns", "calls", "hbm_bytes_per_launch", "hbm_fetch_bytes", "hbm_write_bytes",
         "valu_lane_utilization", "valu_insts_per_wave", "valu_issue_frac", "clock_mhz", "wait_inst_frac",
-        "wait_any_frac", "lds_bank_conflict_frac", "tcc_hit_rate", "tcp_to_tcc_frac")
+        "wait_any_frac", "lds_bank_conflict_frac", "tcc_hit_rate", "tcp_to_tcc_frac", "valu_busy_est",
+        "valu_cycles_per_inst_est", "valu_mix")
 
 
 def main():

@@ -30,9 +30,12 @@ constexpr int ITERS = 65536, CHAINS = 8, UNROLL = 4;
 
 DEF_OP(v_xor_b32, uint32_t, i * 2654435761u, asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a) : "v"(b)))
 DEF_OP(v_add_f32, float, 1.0f + i * 1e-7f, asm volatile("v_add_f32 %0, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_mul_f32, float, 1.0f + i * 1e-7f, asm volatile("v_mul_f32 %0, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_cvt_f32_u32, uint32_t, i, asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(a)))
 DEF_OP(v_fma_f32, float, 1.0f + i * 1e-7f, asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(a) : "v"(b)))
 DEF_OP(v_pk_fma_f32, f32x2, (f32x2{1.0f, 2.0f}), asm volatile("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(a) : "v"(b)))
 DEF_OP(v_fma_f64, double, 1.0 + i * 1e-9, asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_mul_f64, double, 1.0 + i * 1e-9, asm volatile("v_mul_f64 %0, %1, %0" : "+v"(a) : "v"(b)))
 DEF_OP(v_mul_lo_u32, uint32_t, i | 1u, asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(a) : "v"(b)))
 DEF_OP(v_mad_u64_u32, uint64_t, (uint64_t)i, { uint64_t c; asm volatile("v_mad_u64_u32 %0, %1, %2, %2, %0" : "+v"(a), "=s"(c) : "v"((uint32_t)b)); })
 DEF_OP(v_bitop3_b32, uint32_t, i * 2654435761u, asm volatile("v_bitop3_b32 %0, %1, %0, %1 bitop3:0x96" : "+v"(a) : "v"(b)))
@@ -75,7 +78,7 @@ __global__ void __launch_bounds__(256) bench(uint64_t* out, uint32_t* sink) {
 
 template <class Op>
 void run(int cus) {
-    for (int W : {1, 2, 4, 8}) {
+    for (int W : {1, 4, 8}) {
         const int blocks = cus * W, waves = blocks * 4;
         uint64_t* d;
         uint32_t* s;
@@ -120,9 +123,12 @@ int main() {
     printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", prop.gcnArchName, cus, prop.clockRate);
     run<v_xor_b32>(cus);
     run<v_add_f32>(cus);
+    run<v_mul_f32>(cus);
+    run<v_cvt_f32_u32>(cus);
     run<v_fma_f32>(cus);
     run<v_pk_fma_f32>(cus);
     run<v_fma_f64>(cus);
+    run<v_mul_f64>(cus);
     run<v_mul_lo_u32>(cus);
     run<v_mad_u64_u32>(cus);
     run<v_bitop3_b32>(cus);

@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nrt.lib().nrt_abi_version() == 2
+    assert nrt.lib().nrt_abi_version() == 3
 
 
 def test_camera_builder_default_and_build():
@@ -136,3 +136,32 @@ def test_coplanar_ties_detected(scene, pairs, list_ok):
     st = s.stats()
     assert st["coplanar_pairs"] == pairs
     assert st["world_list_ok"] == list_ok
+
+
+@pytest.mark.parametrize("scene,mode", [
+    ("scenes/cornell-box-scene.json", 1),   # 18 quads: every primitive, no boxes (NRT_EXACT_ALL)
+    ("scenes/scale.json", 1),
+    ("scenes/utah-teapot-scene.json", 2),   # 7520 triangles under one instance: world-BVH culling
+    ("scenes/spheres.toml", 2),             # 488 spheres, no instances
+])
+def test_exact_mode(scene, mode):
+    """The reference-exact kernel's traversal (nrt.h nrt_exact_mode): small scenes test every
+    primitive in the reference's depth-first order; large ones cull with the f32 world BVH,
+    each of whose slots maps onto the reference primitive and instance it came from."""
+    from helpers import in_golden
+
+    with in_golden():
+        s = nrt.Scene.load(scene, nrt.CameraConfig(width=8, height=8, samples_per_pixel=1))
+    assert s.stats()["exact_mode"] == mode
+
+
+def test_exact_mode_nested_instances_keep_the_reference_tree():
+    """Nested instances have no single object-space ray per primitive: the exact kernel keeps
+    the reference tree (NRT_EXACT_BVH) once the scene is too large for the all-primitives walk."""
+    b = nrt.Builder()
+    m = b.lambertian(b.solid((0.5, 0.5, 0.5)))
+    quads = [b.quad((i, 0, 0), (0.5, 0, 0), (0, 0.5, 0), m) for i in range(60)]
+    inner = b.translate(b.bvh(quads), (0.0, 1.0, 0.0))
+    outer = b.rotate("y", b.bvh([inner]), 0.25)
+    s = b.finish(b.bvh([outer]))
+    assert s.stats()["exact_mode"] == 0
