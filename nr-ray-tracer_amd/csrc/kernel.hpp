@@ -1565,7 +1565,10 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // variants that need it: it would raise the register budget of every other scene),
 // KF_FLAT = world-list scene without spheres whose materials all have solid colours
 // (no f64 sphere test, uv mapping or texture lookup compiled in: the Cornell box).
-constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4;
+constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8;
+// KF_PLANES (f64 / ChaCha8 only): the scene has no spheres.  The f64 kernel is register-bound;
+// plane-only scenes run best at 4 waves per SIMD (C5 245 ms, C4 33 ms; 3 waves: 267, 35.5),
+// sphere scenes (f64 quadratic, uv, textures) at 3 (C3 earth 4.85 ms against 5.98 at 4).
 
 // Philox sample pool: LDS slots per wave (a power of two; see the Philox branch of
 // render_kernel) and the pool's LDS bytes per workgroup for P pixels per group.
@@ -1593,9 +1596,12 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #define NRT_FLAT_WAVES NRT_WORLD_LIST_WAVES
 #endif
 #ifndef NRT_F64_WAVES
-#define NRT_F64_WAVES 4  // f64 kernels: 4 waves per SIMD (C5 410 -> 274 ms, C4 248 -> 158 ms; 3, 5, 6 slower)
+#define NRT_F64_WAVES 4  // f64 kernels, plane-only scenes (KF_PLANES): 4 waves per SIMD
 #endif
-    if (sizeof(R) == 8) return NRT_F64_WAVES;
+#ifndef NRT_F64_SPHERE_WAVES
+#define NRT_F64_SPHERE_WAVES 3
+#endif
+    if (sizeof(R) == 8) return (kflags & KF_PLANES) ? NRT_F64_WAVES : NRT_F64_SPHERE_WAVES;
 #ifndef NRT_WBVH_WAVES
 #define NRT_WBVH_WAVES 1
 #endif

@@ -7,11 +7,11 @@
 namespace nrt {
 
 void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, int maxd, bool perlin,
-                  hipStream_t stream) {
+                  bool planes, hipStream_t stream) {
     const bool deep = maxd > 1;
     if (rng == RNG_CHACHA8) {
         if (deep) launch_one<double, dev::ChaCha8, MAX_INSTANCE_DEPTH, true>(p, v, perlin, stream);
-        else launch_one<double, dev::ChaCha8, 1, true>(p, v, perlin, stream);
+        else launch_one<double, dev::ChaCha8, 1, true>(p, v, perlin, stream, false, planes);
     } else {
         if (deep) launch_one<double, dev::Philox, MAX_INSTANCE_DEPTH, true>(p, v, perlin, stream);
         else launch_one<double, dev::Philox, 1, true>(p, v, perlin, stream);

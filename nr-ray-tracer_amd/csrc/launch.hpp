@@ -19,7 +19,7 @@ constexpr int MODE_WORLD_BVH = -1;
 // perlin: the scene has Noise / Marble textures (selects the KF_PERLIN kernel variants);
 // flat: no spheres and only solid-colour textures (the KF_FLAT world-list / world-BVH variants)
 void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t rng, int maxd, bool perlin,
-                  hipStream_t stream);
+                  bool planes, hipStream_t stream);
 void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, int maxd, bool perlin, bool flat,
                  hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,

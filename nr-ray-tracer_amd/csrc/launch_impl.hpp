@@ -64,7 +64,7 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
 
 template <typename R, class G, int MAXD, bool EXACT>
 static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perlin, hipStream_t stream,
-                       bool flat = false) {
+                       bool flat = false, bool planes = false) {
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
@@ -84,6 +84,13 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
             } else {
                 launch_variant<R, G, MAXD, EXACT, false, KF_FLAT>(p, v, ring, stream);
             }
+            return;
+        }
+    }
+    if constexpr (sizeof(R) == 8 && MAXD == 1 && G::exact_stream) {
+        if (planes && !perlin && !p.counters) {  // KF_PLANES: the 4-wave f64 variant
+            if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES>(p, v, ring + scene, stream);
+            else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES>(p, v, ring, stream);
             return;
         }
     }

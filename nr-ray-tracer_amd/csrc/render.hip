@@ -50,6 +50,7 @@ struct DeviceScene {
     uint64_t world_units = 0;
     bool wbvh_ok = false;   // world BVH available (v32.wbvh + wbvh_prims)
     bool perlin = false;    // Noise / Marble textures present (KF_PERLIN kernel variants)
+    bool planes = false;    // no spheres (the f64 kernel's KF_PLANES variant)
     bool flat = false;      // world list without spheres, solid colours only (KF_FLAT variants)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
@@ -143,6 +144,8 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr};
         ds->wbvh_ok = fs.wbvh_ok;
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
+        ds->planes = !fs.prims.empty();
+        for (const DPrim<double>& pr : fs.prims) ds->planes &= pr.kind != PRIM_SPHERE;
         ds->flat = !ds->perlin;
         for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
         // unit kinds from the runs (box / room units also hold header and empty face slots)
@@ -212,7 +215,8 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;
         check(hipMemsetAsync(q.queue, 0, qwords * sizeof(unsigned int), stream), "hipMemsetAsync(queue)");
     }
-    if (precision == 0) launch_exact(q, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, ds->perlin, stream);
+    if (precision == 0)
+        launch_exact(q, ds->v64, rng, ds->v64.max_depth > 1 ? MAX_INSTANCE_DEPTH : 1, ds->perlin, ds->planes, stream);
     else {
         const int maxd = gpu_fast_maxd(ds, trace);
         DSceneView<float> v = ds->v32;  // stage (LDS) only the tables this mode reads

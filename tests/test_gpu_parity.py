@@ -215,3 +215,28 @@ def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
     b = s.render(precision="f64", rng="chacha8")
     mismatch = np.mean(np.abs(a - b).max(axis=2) > 1e-3 + 1e-3 * np.abs(b).max(axis=2))
     assert mismatch <= 0.01, mismatch
+
+
+@pytest.mark.parametrize("scene,w,h,spp", [
+    ("scenes/cornell-box-scene.json", 40, 32, 4),
+    ("scenes/utah-teapot-scene.json", 32, 24, 2),
+    ("scenes/spheres.toml", 48, 27, 4),
+    ("scenes/cube-scene.json", 40, 30, 4),   # touching coplanar cube faces: exact ties by rank
+])
+def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
+    """The three traversals of the reference-exact kernel (nrt.h nrt_exact_mode: the reference
+    tree, every primitive in depth-first order, f32 world-BVH culling with the reference tests)
+    find the same closest hit with the same tie-break, so the f64/ChaCha8 frames are equal bit
+    for bit (BVH::hit, object.rs:89-121)."""
+    s = load(scene, w, h, spp)
+    frames = {}
+    for name, env in {"bvh": ("0", "0"), "all": ("1", "0"), "world": ("0", "1")}.items():
+        if name == "world" and s.stats()["exact_mode"] != 2:
+            continue
+        monkeypatch.setenv("NRT_EXACT_ALL", env[0])
+        monkeypatch.setenv("NRT_EXACT_WBVH", env[1])
+        frames[name] = s.render(precision="f64", rng="chacha8")
+    base = frames.pop("bvh")
+    assert np.isfinite(base).all()
+    for name, img in frames.items():
+        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name

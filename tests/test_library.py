@@ -139,15 +139,15 @@ def test_coplanar_ties_detected(scene, pairs, list_ok):
 
 
 @pytest.mark.parametrize("scene,mode", [
-    ("scenes/cornell-box-scene.json", 1),   # 18 quads: every primitive, no boxes (NRT_EXACT_ALL)
-    ("scenes/scale.json", 1),
+    ("scenes/cornell-box-scene.json", 2),   # world-BVH culling wherever the slots map
+    ("scenes/scale.json", 2),
     ("scenes/utah-teapot-scene.json", 2),   # 7520 triangles under one instance: world-BVH culling
     ("scenes/spheres.toml", 2),             # 488 spheres, no instances
 ])
 def test_exact_mode(scene, mode):
-    """The reference-exact kernel's traversal (nrt.h nrt_exact_mode): small scenes test every
-    primitive in the reference's depth-first order; large ones cull with the f32 world BVH,
-    each of whose slots maps onto the reference primitive and instance it came from."""
+    """The reference-exact kernel's traversal (nrt.h nrt_exact_mode): the f32 world BVH culls,
+    each of its slots mapped onto the reference primitive and instance it came from; small
+    scenes without that mapping test every primitive in depth-first order."""
     from helpers import in_golden
 
     with in_golden():
@@ -155,13 +155,15 @@ def test_exact_mode(scene, mode):
     assert s.stats()["exact_mode"] == mode
 
 
-def test_exact_mode_nested_instances_keep_the_reference_tree():
-    """Nested instances have no single object-space ray per primitive: the exact kernel keeps
-    the reference tree (NRT_EXACT_BVH) once the scene is too large for the all-primitives walk."""
+@pytest.mark.parametrize("n,mode", [(60, 0), (10, 1)])
+def test_exact_mode_nested_instances(n, mode):
+    """Nested instances have no single object-space ray per primitive: no world-BVH mapping, so
+    the exact kernel walks every primitive (small scenes, NRT_EXACT_ALL) or keeps the reference
+    tree (NRT_EXACT_BVH)."""
     b = nrt.Builder()
     m = b.lambertian(b.solid((0.5, 0.5, 0.5)))
-    quads = [b.quad((i, 0, 0), (0.5, 0, 0), (0, 0.5, 0), m) for i in range(60)]
+    quads = [b.quad((i, 0, 0), (0.5, 0, 0), (0, 0.5, 0), m) for i in range(n)]
     inner = b.translate(b.bvh(quads), (0.0, 1.0, 0.0))
     outer = b.rotate("y", b.bvh([inner]), 0.25)
     s = b.finish(b.bvh([outer]))
-    assert s.stats()["exact_mode"] == 0
+    assert s.stats()["exact_mode"] == mode
