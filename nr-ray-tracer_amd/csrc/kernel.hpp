@@ -488,7 +488,7 @@ __device__ __forceinline__ R fast_prim_t(const DPrimFast<R>& q, const Ray<R>& r,
 }
 
 // ray into object space through an instance's chain (outer -> inner)
-template <typename R, bool EXACT>
+template <typename R, bool EXACT, bool PREP = true>  // PREP: 1/d for slab tests (not needed by prim tests)
 __device__ __forceinline__ void xform_in(const DSceneView<R>& sc, const DInstance& inst, Ray<R>& r) {
     for (uint32_t k = 0; k < inst.num_xforms; ++k) {
         const DXform<R>& x = sc.xforms[inst.first_xform + k];
@@ -502,7 +502,7 @@ __device__ __forceinline__ void xform_in(const DSceneView<R>& sc, const DInstanc
             r.d = xf_vector(x.m, r.d);
         }
     }
-    prep_ray<R, EXACT>(r);
+    if constexpr (PREP) prep_ray<R, EXACT>(r);
 }
 
 template <typename R>
@@ -875,16 +875,36 @@ __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc,
     else wbvh_leaf_t<R, FLAT, false>(ts, sc, ray, ref, pc);
 }
 
-// Stacks: LDS, entry k of this lane at stack[k * BLOCK] (STRIDE = BLOCK), or a private
-// array (STRIDE = 1: the exact kernel's world-BVH mode, whose LDS holds the ChaCha8 ring).
-template <int STRIDE = BLOCK>
-__device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, const int32_t* stack) {
-    return ts.sp ? stack[(--ts.sp) * STRIDE] : WBVH_DONE;
+// Traversal stacks.  f32 kernels: LDS, entry k of this lane at stack[k * BLOCK].  The exact
+// kernel's world-BVH mode (its LDS holds the ChaCha8 ring and the staged scene): a private
+// array (scratch), optionally below a short LDS stack of NRT_SHORT_STACK entries.  Measured:
+// 8 LDS entries, paid for by not staging the scene, ran slower on every config (C5 245 ->
+// 323 ms, C4 400 -> 473 ms, C3 5.0 -> 6.0 ms), so the LDS part is off.
+#ifndef NRT_SHORT_STACK
+#define NRT_SHORT_STACK 0
+#endif
+constexpr uint32_t SHORT_STACK = NRT_SHORT_STACK;
+struct ShortStack {
+    int32_t* lds;  // this lane's entry 0; entry k at lds[k * BLOCK]
+    int32_t ovf[WBVH_STACK + 1 - SHORT_STACK];
+};
+__device__ __forceinline__ void stk_write(int32_t* s, uint32_t k, int32_t v) { s[k * BLOCK] = v; }
+__device__ __forceinline__ int32_t stk_read(int32_t* s, uint32_t k) { return s[k * BLOCK]; }
+__device__ __forceinline__ void stk_write(ShortStack& s, uint32_t k, int32_t v) {
+    if (SHORT_STACK > 0 && k < SHORT_STACK) s.lds[k * BLOCK] = v;
+    else s.ovf[k - SHORT_STACK] = v;
+}
+__device__ __forceinline__ int32_t stk_read(ShortStack& s, uint32_t k) {
+    return (SHORT_STACK > 0 && k < SHORT_STACK) ? s.lds[k * BLOCK] : s.ovf[k - SHORT_STACK];
+}
+template <class STK>
+__device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, STK& stack) {
+    return ts.sp ? stk_read(stack, --ts.sp) : WBVH_DONE;
 }
 
 // Binary node visit: both child boxes, nearer hit child next, the other pushed.
-template <typename R, int STRIDE = BLOCK>
-__device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
+template <typename R, class STK>
+__device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
     const DBvhNode nd = load16(sc.wbvh + t.node);
     const float a0x = nd.lo0[0] * t.ix - t.ox, b0x = nd.hi0[0] * t.ix - t.ox;
     const float a0y = nd.lo0[1] * t.iy - t.oy, b0y = nd.hi0[1] * t.iy - t.oy;
@@ -899,12 +919,12 @@ __device__ __forceinline__ void wbvh2_visit(WbvhTrav& t, const DSceneView<R>& sc
     const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
     if (h0 && h1) {
         const bool near0 = tn0 <= tn1;
-        stack[(t.sp++) * STRIDE] = near0 ? nd.c1 : nd.c0;
+        stk_write(stack, t.sp++, near0 ? nd.c1 : nd.c0);
         t.node = near0 ? nd.c0 : nd.c1;
     } else if (h0 || h1) {
         t.node = h0 ? nd.c0 : nd.c1;
     } else {
-        t.node = wbvh_pop<STRIDE>(t, stack);
+        t.node = wbvh_pop(t, stack);
     }
 }
 
@@ -919,8 +939,8 @@ __device__ __forceinline__ void wbvh_cswap(float& ta, int32_t& ca, float& tb, in
     tb = sw ? t0 : tb;
     cb = sw ? c0 : cb;
 }
-template <typename R, int STRIDE = BLOCK>
-__device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc, int32_t* stack) {
+template <typename R, class STK>
+__device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
     const DBvh4Node nd = load16(sc.wbvh4 + t.node);
     // plane t = (org + q * step - o) / d = q * (step / d) + (org / d - o / d)
     const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
@@ -958,13 +978,13 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
 #endif
     // branch-free pushes: every slot is written at sp, sp advances past the hit ones (the
     // stack has one spare entry above the tree's bound for the writes that do not count)
-    stack[t.sp * STRIDE] = c3;
+    stk_write(stack, t.sp, c3);
     t.sp += t3 != INFINITY ? 1u : 0u;
-    stack[t.sp * STRIDE] = c2;
+    stk_write(stack, t.sp, c2);
     t.sp += t2 != INFINITY ? 1u : 0u;
-    stack[t.sp * STRIDE] = c1;
+    stk_write(stack, t.sp, c1);
     t.sp += t1 != INFINITY ? 1u : 0u;
-    t.node = t0 != INFINITY ? c0 : wbvh_pop<STRIDE>(t, stack);
+    t.node = t0 != INFINITY ? c0 : wbvh_pop(t, stack);
 }
 
 // One round: descend through inner nodes until the lane holds a leaf (or is
@@ -1200,24 +1220,26 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 // visiting order does not matter.  The culling is conservative: the f32 boxes are rounded
 // outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
 // inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
-// private array (the LDS holds the ChaCha8 ring).
+// short LDS stack with a private overflow (ShortStack; the LDS holds the ChaCha8 ring).
 template <typename R, int MAXD>
-__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
+                                                 int32_t* lds_stack) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
     fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), fr);
-    int32_t stk[WBVH_STACK + 1];
+    ShortStack stk;
+    stk.lds = lds_stack;
     R best_t = R(INFINITY);
     uint32_t best_rank = 0;
     int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
     Ray<R> oray = wray;
     while (true) {
         while (ts.node >= 0) {
-            if (sc.wbvh4) wbvh4_visit<R, 1>(ts, sc, stk);
-            else wbvh2_visit<R, 1>(ts, sc, stk);
+            if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
+            else wbvh2_visit<R>(ts, sc, stk);
         }
         if (ts.node == WBVH_DONE) break;
         const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
@@ -1225,7 +1247,7 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
             const DExactRef ref = sc.wexact[first + k];
             if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
                 oray = wray;
-                if (ref.inst >= 0) xform_in<R, true>(sc, sc.instances[ref.inst], oray);
+                if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
                 cur_inst = ref.inst;
             }
             const DPrim<R>& pr = sc.prims[ref.prim];
@@ -1245,7 +1267,7 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
                 ts.t_best = (float)best_t * (1.0f + 0x1p-20f);
             }
         }
-        ts.node = wbvh_pop<1>(ts, stk);
+        ts.node = wbvh_pop(ts, stk);
     }
     hm.t = best_t;
     hm.prim = (uint32_t)best_prim;
@@ -1260,7 +1282,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
-        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm, stack);
         return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
     } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
@@ -1659,8 +1681,12 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
-    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t) : 0u;
-    int32_t* stack = MAXD < 0 ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
+    // world-BVH stack: f32 kernels the tree's bound + 1 entries; the exact kernel's world-BVH mode
+    // a short stack (SHORT_STACK entries, overflow in scratch)
+    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t)
+                                 : (EXACT && SHORT_STACK && p.exact_wbvh) ? SHORT_STACK * BLOCK * (uint32_t)sizeof(int32_t)
+                                                                         : 0u;
+    int32_t* stack = stack_bytes ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
 
