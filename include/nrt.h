@@ -143,6 +143,9 @@ typedef void (*nrt_progress_fn)(void* user, uint64_t pixels_done);
 
 /* ---- library ---------------------------------------------------------- */
 int nrt_abi_version(void);
+/* sha256 prefix of the library's sources it was built from (build provenance; no reference
+ * counterpart) */
+const char* nrt_build_id(void);
 const char* nrt_last_error(void);   /* thread-local; message text mirrors anyhow's */
 int nrt_device_count(void);
 

@@ -299,6 +299,11 @@ void device_zero(void* p, size_t bytes, int device);
 extern "C" {
 
 int nrt_abi_version(void) { return NRT_ABI_VERSION; }
+
+#ifndef NRT_SRC_HASH
+#define NRT_SRC_HASH "unknown"
+#endif
+const char* nrt_build_id(void) { return NRT_SRC_HASH; }
 const char* nrt_last_error(void) { return g_last_error.c_str(); }
 int nrt_device_count(void) { return gpu_device_count(); }
 

@@ -79,6 +79,7 @@ PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
 _D3 = C.POINTER(C.c_double)
 SIGNATURES = {
     "nrt_abi_version": (C.c_int, []),
+    "nrt_build_id": (C.c_char_p, []),
     "nrt_last_error": (C.c_char_p, []),
     "nrt_device_count": (C.c_int, []),
     "nrt_camera_builder_default": (None, [C.POINTER(_CameraBuilder)]),
@@ -171,6 +172,28 @@ def _d3(v: Sequence[float]):
 
 def device_count() -> int:
     return lib().nrt_device_count()
+
+
+def build_id() -> str:
+    """sha256 prefix of the sources the loaded libnrt.so was built from (nrt_build_id)."""
+    return lib().nrt_build_id().decode()
+
+
+def source_hash(pkg_dir: Optional[str] = None) -> str:
+    """The same hash over the sources in this tree (Makefile SRC_HASH: csrc/*.cpp, *.hpp, *.hip
+    in byte-wise sorted order, then include/nrt.h)."""
+    import glob
+    import hashlib
+
+    pkg = pkg_dir or os.path.dirname(_HERE)
+    files = sorted(sum((glob.glob(os.path.join("csrc", ext), root_dir=pkg) for ext in ("*.cpp", "*.hpp", "*.hip")), []))
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(pkg, "..", "include", "nrt.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 @dataclass

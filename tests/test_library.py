@@ -167,3 +167,9 @@ def test_exact_mode_nested_instances(n, mode):
     outer = b.rotate("y", b.bvh([inner]), 0.25)
     s = b.finish(b.bvh([outer]))
     assert s.stats()["exact_mode"] == mode
+
+
+def test_library_built_from_these_sources():
+    """Build provenance: the loaded libnrt.so carries the hash of the sources it was
+    compiled from; it must equal the hash of csrc/ + include/nrt.h in this tree."""
+    assert nrt.build_id() == nrt.source_hash()
