@@ -60,14 +60,7 @@ struct alignas(16) DPrim {
     Real s;     // sphere: radius           plane: d = normal.p
     uint32_t kind;
     uint32_t material;
-    // Planes whose u and v each lie on one coordinate axis (exact zeros elsewhere, so normal and
-    // w do too): PLANE_AXES | a | i << 2 | j << 4 with a = the normal's axis, i = u's, j = v's;
-    // the exact kernel then evaluates Plane::hit's dots and crosses on the nonzero terms only
-    // (plane_t_axes: the same roundings, zeros aside).  0 otherwise.
-    uint32_t axes;
-    uint32_t pad;
 };
-constexpr uint32_t PLANE_AXES = 1u << 8;
 
 // Fast kernel primitive (64 B in f32).  Plane: alpha = (point-p).(v x w),
 // beta = (point-p).(w x u) (scalar triple products of plane.rs:156-157), so

@@ -108,23 +108,6 @@ struct Flattener {
 
     static void set3(double* dst, V3 v) { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; }
 
-    // DPrim::axes: u on axis i, v on axis j != i, the normal and w on the third axis a, every
-    // other component an exact (signed) zero; 0 when any of that fails.
-    static uint32_t plane_axes(const DPrim<double>& p) {
-        auto axis = [](const double* x) {
-            int k = -1;
-            for (int c = 0; c < 3; ++c) {
-                if (x[c] == 0.0) continue;
-                if (k >= 0 || !std::isfinite(x[c])) return -1;
-                k = c;
-            }
-            return k;
-        };
-        const int i = axis(p.b), j = axis(p.c), a = axis(p.n), aw = axis(p.w);
-        if (i < 0 || j < 0 || a < 0 || i == j || a == i || a == j || aw != a) return 0u;
-        return PLANE_AXES | (uint32_t)a | (uint32_t)i << 2 | (uint32_t)j << 4;
-    }
-
     uint32_t prim(const Object* o, const MaterialPtr& mat) {
         auto it = prim_ids.find(o);
         if (it != prim_ids.end()) return it->second;
@@ -142,7 +125,6 @@ struct Flattener {
             set3(p.n, o->normal);
             set3(p.w, o->w);
             p.s = o->d;
-            p.axes = plane_axes(p);
         }
         p.material = material(mat);
         const uint32_t id = (uint32_t)out.prims.size();
@@ -1173,8 +1155,6 @@ FlatScene32 to_f32(const FlatScene& s) {
         b.s = (float)a.s;
         b.kind = a.kind;
         b.material = a.material;
-        b.axes = a.axes;
-        b.pad = 0;
     }
     o.xforms.resize(s.xforms.size());
     for (size_t i = 0; i < s.xforms.size(); ++i) {

@@ -39,7 +39,10 @@ constexpr int BLOCK = 256;
 #define NRT_WBVH_SORT 0  // 4-wide visits: 1 = full sorting network; 0 = nearest hit child first, the rest in slot order (C4 +4 %)
 #endif
 #ifndef NRT_WBVH_IFIF
-#define NRT_WBVH_IFIF 0  // world BVH: one node visit or one primitive per lane and trip (wbvh_trip)
+// world BVH: one node visit or one primitive per lane and trip (wbvh_trip) in the KF_FLAT
+// variant (triangles / quads only: a primitive costs a fifth of a visit; C4 6 307 -> 6 400
+// Msamples/s); scenes with f64 sphere tests keep the speculative rounds (C1 -27 % if-if)
+#define NRT_WBVH_IFIF 1
 #endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 
@@ -456,40 +459,6 @@ __device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alph
     const V<R> ph = point - ld3(q.a);
     alpha = dot(ld3(q.w), cross(ph, ld3(q.c)));
     beta = dot(ld3(q.w), cross(ld3(q.b), ph));
-    bool inside;
-    if (q.kind == PRIM_QUAD)
-        inside = (R(0) <= alpha && alpha <= R(1)) && (R(0) <= beta && beta <= R(1));
-    else
-        inside = alpha > R(0) && beta > R(0) && (alpha + beta) < R(1);
-    return inside ? t : R(-1);
-}
-
-// Plane::hit (plane.rs:141-174) for a plane with DPrim::axes set: u = Lu e_i, v = Lv e_j and the
-// normal and w on axis a, every other component an exact zero.  glam's dots are left-to-right
-// sums and its cross products differences of products, so each of Plane::hit's dots and the
-// a-th components of its crosses reduces to one rounded product (the zero terms add signed
-// zeros only): denom = n_a d_a, n.o = n_a o_a, (ph x v)_a = ph_{a+1} Lv if j = a+2, else
-// -(Lv ph_{a+2}); (u x ph)_a = Lu ph_{a+2} if i = a+1, else -(ph_{a+1} Lu); alpha and beta are
-// w_a times those.  Same t, same hit decision as plane_t (a zero's sign cannot change
-// 0 <= alpha or t >= 0.001), at a quarter of its f64 operations.
-template <typename R>
-__device__ __forceinline__ R plane_t_axes(const DPrim<R>& q, const Ray<R>& r) {
-    const uint32_t a = q.axes & 3u, i = (q.axes >> 2) & 3u, j = (q.axes >> 4) & 3u;
-    const uint32_t a1 = a == 2u ? 0u : a + 1u, a2 = a == 0u ? 2u : a - 1u;  // a + 1, a + 2 (mod 3)
-    auto comp = [](const R* v, uint32_t k) { return k == 0u ? v[0] : (k == 1u ? v[1] : v[2]); };
-    const R* o = &r.o.x;
-    const R* d = &r.d.x;
-    const R na = comp(q.n, a);
-    const R denom = na * comp(d, a);
-    if (fabs(denom) < R(1e-8)) return R(-1);
-    const R t = (q.s - na * comp(o, a)) / denom;
-    if (!(R(0.001) <= t && t <= R(INFINITY))) return R(-1);
-    const R ph1 = (comp(o, a1) + t * comp(d, a1)) - comp(q.a, a1);  // ray.at(t) - p, components a+1, a+2
-    const R ph2 = (comp(o, a2) + t * comp(d, a2)) - comp(q.a, a2);
-    const R lv = comp(q.c, j), lu = comp(q.b, i), wa = comp(q.w, a);
-    const R ca = j == a2 ? ph1 * lv : -(lv * ph2);
-    const R cb = i == a1 ? lu * ph2 : -(ph1 * lu);
-    const R alpha = wa * ca, beta = wa * cb;
     bool inside;
     if (q.kind == PRIM_QUAD)
         inside = (R(0) <= alpha && alpha <= R(1)) && (R(0) <= beta && beta <= R(1));
@@ -1058,7 +1027,7 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
 #endif
 }
 
-// "If-if" trip (NRT_WBVH_IFIF): every busy lane does exactly one unit of work per trip,
+// "If-if" trip (NRT_WBVH_IFIF, KF_FLAT): every busy lane does exactly one unit of work per trip,
 // one primitive of its current leaf or, without a leaf, one node visit; a leaf that a visit
 // or a pop turns up becomes the lane's leaf cursor at once (the leaf ref, advanced in place:
 // first + 1, count - 1).  Lanes never wait for the wave to finish a phase, so long and
@@ -1111,13 +1080,13 @@ __device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
 template <typename R, bool FLAT = false>
 __device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack,
                                           unsigned long long* pc = nullptr) {
-#if NRT_WBVH_IFIF
-    if (sc.wbvh4) wbvh_trip<R, true, FLAT>(ts, sc, ray, stack, pc);
-    else wbvh_trip<R, false, FLAT>(ts, sc, ray, stack, pc);
-#else
-    if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack, pc);
-    else wbvh_round<R, FLAT>(ts, sc, ray, stack, pc);
-#endif
+    if constexpr (FLAT && NRT_WBVH_IFIF) {
+        if (sc.wbvh4) wbvh_trip<R, true, FLAT>(ts, sc, ray, stack, pc);
+        else wbvh_trip<R, false, FLAT>(ts, sc, ray, stack, pc);
+    } else {
+        if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack, pc);
+        else wbvh_round<R, FLAT>(ts, sc, ray, stack, pc);
+    }
 }
 
 template <typename R, int MAXD, bool FLAT = false>
@@ -1189,8 +1158,6 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
                 const DPrim<R>& pr = sc.prims[pid];
                 if (pr.kind == PRIM_SPHERE) {
                     t = sphere_t(pr, ray);
-                } else if (pr.axes) {
-                    t = plane_t_axes(pr, ray);
                 } else {
                     R alpha, beta;
                     V<R> point;
@@ -1290,8 +1257,6 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
             R t;
             if (pr.kind == PRIM_SPHERE) {
                 t = sphere_t(pr, oray);
-            } else if (pr.axes) {
-                t = plane_t_axes(pr, oray);
             } else {
                 R alpha, beta;
                 V<R> point;
