@@ -32,9 +32,6 @@ constexpr int BLOCK = 256;
 #ifndef NRT_SPECULATIVE
 #define NRT_SPECULATIVE 1  // world-BVH rounds: lanes holding a leaf keep descending (Aila & Laine)
 #endif
-#ifndef NRT_CAM_RELOAD
-#define NRT_CAM_RELOAD 0
-#endif
 #ifndef NRT_WBVH_SORT
 #define NRT_WBVH_SORT 0  // 4-wide visits: 1 = full sorting network; 0 = nearest hit child first, the rest in slot order (C4 +4 %)
 #endif
@@ -879,27 +876,16 @@ __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc,
 }
 
 // Traversal stacks.  f32 kernels: LDS, entry k of this lane at stack[k * BLOCK].  The exact
-// kernel's world-BVH mode (its LDS holds the ChaCha8 ring and the staged scene): a private
-// array (scratch), optionally below a short LDS stack of NRT_SHORT_STACK entries.  Measured:
-// 8 LDS entries, paid for by not staging the scene, ran slower on every config (C5 245 ->
-// 323 ms, C4 400 -> 473 ms, C3 5.0 -> 6.0 ms), so the LDS part is off.
-#ifndef NRT_SHORT_STACK
-#define NRT_SHORT_STACK 0
-#endif
-constexpr uint32_t SHORT_STACK = NRT_SHORT_STACK;
-struct ShortStack {
-    int32_t* lds;  // this lane's entry 0; entry k at lds[k * BLOCK]
-    int32_t ovf[WBVH_STACK + 1 - SHORT_STACK];
+// kernel's world-BVH mode: a private array (scratch), because its LDS holds the ChaCha8 ring
+// and the staged scene (an 8-entry LDS part, paid for by not staging the scene, measured
+// slower on every f64 config: C5 245 -> 323 ms, C4 400 -> 473 ms, C3 5.0 -> 6.0 ms).
+struct PrivStack {
+    int32_t e[WBVH_STACK + 1];
 };
 __device__ __forceinline__ void stk_write(int32_t* s, uint32_t k, int32_t v) { s[k * BLOCK] = v; }
 __device__ __forceinline__ int32_t stk_read(int32_t* s, uint32_t k) { return s[k * BLOCK]; }
-__device__ __forceinline__ void stk_write(ShortStack& s, uint32_t k, int32_t v) {
-    if (SHORT_STACK > 0 && k < SHORT_STACK) s.lds[k * BLOCK] = v;
-    else s.ovf[k - SHORT_STACK] = v;
-}
-__device__ __forceinline__ int32_t stk_read(ShortStack& s, uint32_t k) {
-    return (SHORT_STACK > 0 && k < SHORT_STACK) ? s.lds[k * BLOCK] : s.ovf[k - SHORT_STACK];
-}
+__device__ __forceinline__ void stk_write(PrivStack& s, uint32_t k, int32_t v) { s.e[k] = v; }
+__device__ __forceinline__ int32_t stk_read(PrivStack& s, uint32_t k) { return s.e[k]; }
 template <class STK>
 __device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, STK& stack) {
     return ts.sp ? stk_read(stack, --ts.sp) : WBVH_DONE;
@@ -1223,18 +1209,16 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 // visiting order does not matter.  The culling is conservative: the f32 boxes are rounded
 // outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
 // inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
-// short LDS stack with a private overflow (ShortStack; the LDS holds the ChaCha8 ring).
+// private array (PrivStack; the LDS holds the ChaCha8 ring and the staged scene).
 template <typename R, int MAXD>
-__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                                 int32_t* lds_stack) {
+__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
     fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), fr);
-    ShortStack stk;
-    stk.lds = lds_stack;
+    PrivStack stk;
     R best_t = R(INFINITY);
     uint32_t best_rank = 0;
     int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
@@ -1285,7 +1269,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
-        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm, stack);
+        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
         return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
     } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
@@ -1684,34 +1668,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
-    // world-BVH stack: f32 kernels the tree's bound + 1 entries; the exact kernel's world-BVH mode
-    // a short stack (SHORT_STACK entries, overflow in scratch)
-    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t)
-                                 : (EXACT && SHORT_STACK && p.exact_wbvh) ? SHORT_STACK * BLOCK * (uint32_t)sizeof(int32_t)
-                                                                         : 0u;
+    // world-BVH stack (f32 kernels): the tree's bound + 1 entries
+    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t) : 0u;
     int32_t* stack = stack_bytes ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
 
     G g;
     // Camera vectors (camera.rs:205-227) q = 0..6: top_left, delta_u, delta_v, look_from,
-    // disk_u, disk_v, background.  f32 (NRT_CAM_RELOAD): read from the kernel arguments where
-    // used, through a pointer the compiler cannot see through, so the 21 floats do not hold
-    // SGPRs across the loop (the loop is at the SGPR limit and spills into VGPR lanes).
+    // disk_u, disk_v, background (f32: the host-rounded copies, kernel arguments in SGPRs)
     auto cam = [&](int q) -> V<R> {
-        if constexpr (sizeof(R) == 4 && NRT_CAM_RELOAD) {
-            // the kernel's first argument is `p`: its camf member sits at a fixed kernarg offset
-            using KF = const __attribute__((address_space(4))) float*;
-            KF c = (KF)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
-                        offsetof(RenderParams, camf));
-            asm volatile("" : "+s"(c));
-            return mk(c[3 * q], c[3 * q + 1], c[3 * q + 2]);
-        } else {
-            const double* d = q == 0 ? p.top_left : q == 1 ? p.pixel_delta_u : q == 2 ? p.pixel_delta_v
-                            : q == 3 ? p.look_from : q == 4 ? p.defocus_disk_u : q == 5 ? p.defocus_disk_v
-                            : p.background;
-            return cam3<R>(p, q, d);
-        }
+        const double* d = q == 0 ? p.top_left : q == 1 ? p.pixel_delta_u : q == 2 ? p.pixel_delta_v
+                        : q == 3 ? p.look_from : q == 4 ? p.defocus_disk_u : q == 5 ? p.defocus_disk_v
+                        : p.background;
+        return cam3<R>(p, q, d);
     };
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform values live in SGPRs
 

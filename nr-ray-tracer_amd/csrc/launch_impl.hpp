@@ -68,16 +68,8 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
-                          (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0) +
-                          ((EXACT && MAXD > 0 && dev::SHORT_STACK && p.exact_wbvh)
-                               ? dev::SHORT_STACK * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
-    // (with an LDS short stack the exact world-BVH mode would give up the staged scene for
-    // occupancy: measured slower, see kernel.hpp NRT_SHORT_STACK)
-#ifndef NRT_EXACT_WORLD_LDS_SCENE
-#define NRT_EXACT_WORLD_LDS_SCENE 1
-#endif
-    const bool no_stage = EXACT && MAXD > 0 && p.exact_wbvh && (dev::SHORT_STACK || !NRT_EXACT_WORLD_LDS_SCENE);
-    const uint32_t scene = no_stage ? LDS_SCENE_LIMIT + 1 : lds_scene_bytes(v);
+                          (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
+    const uint32_t scene = lds_scene_bytes(v);
     using dev::KF_FLAT;
     using dev::KF_PERLIN;
     using dev::KF_PROF;
