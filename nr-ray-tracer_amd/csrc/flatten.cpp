@@ -834,6 +834,8 @@ struct Flattener {
     }
     // World BVH over the world primitives (wbvh.hpp); unusable trees (too deep for
     // the kernel's stack) leave wbvh_ok false and the instance BVH in charge.
+    std::vector<std::array<double, 6>> wbounds;  // the world BVH's inputs (exact tree rebuild)
+    std::vector<float> wcost;
     void build_wbvh() {
         std::vector<std::array<double, 6>> bounds(out.wprims.size());
         // SAH weights relative to a (binary) node visit: a plane test; f64 sphere tests cost ~4 of
@@ -875,6 +877,10 @@ struct Flattener {
             out.wbvh_ok = false;
             return;
         }
+        wbounds = bounds;
+        wcost = cost;
+        out.wprims_kind.resize(out.wprims.size());
+        for (size_t i = 0; i < out.wprims.size(); ++i) out.wprims_kind[i] = out.wprims[i].meta & WKIND_MASK;
         out.wbvh_prims.reserve(out.wbvh.order.size());
         for (uint32_t idx : out.wbvh.order) out.wbvh_prims.push_back(out.wprims[idx]);
         out.wbvh_ok = true;
@@ -1058,7 +1064,8 @@ float round_up(double x) {
 // any disagreement in count or kind, leave the mapping empty (mode unavailable).
 static void map_exact_refs(FlatScene& s) {
     s.wexact.clear();
-    if (!s.wbvh_ok || s.wbvh.order.empty()) return;
+    const WorldBvh& tree = s.exact_tree();
+    if (!s.wbvh_ok || tree.order.empty()) return;
     std::vector<std::pair<uint32_t, int32_t>> seq;
     bool ok = true;
     auto walk = [&](int32_t node, int32_t inst, auto&& self) -> void {
@@ -1086,22 +1093,44 @@ static void map_exact_refs(FlatScene& s) {
         }
     };
     walk(s.root, -1, walk);
-    if (!ok || seq.size() != s.wbvh.order.size()) return;
-    std::vector<DExactRef> refs(s.wbvh.order.size());
+    if (!ok || seq.size() != tree.order.size() || seq.size() != s.wbvh.order.size()) return;
+    std::vector<DExactRef> refs(tree.order.size());
     for (size_t slot = 0; slot < refs.size(); ++slot) {
-        const uint32_t rank = s.wbvh.order[slot];
-        if (rank >= seq.size()) return;
+        const uint32_t rank = tree.order[slot];
+        if (rank >= seq.size() || rank >= s.wbvh.order.size()) return;
         const auto& e = seq[rank];
-        if (e.first >= s.prims.size() || s.prims[e.first].kind != (s.wbvh_prims[slot].meta & WKIND_MASK)) return;
+        // kind of world primitive `rank` (the shared tree's slot order is a permutation of it)
+        const uint32_t wkind = rank < s.wprims_kind.size() ? s.wprims_kind[rank] : 0xFFFFFFFFu;
+        if (e.first >= s.prims.size() || s.prims[e.first].kind != wkind) return;
         refs[slot] = DExactRef{e.first, e.second, rank, 0u};
     }
     s.wexact = std::move(refs);
 }
 
+constexpr float EXACT_SAH_PRIM_COST = 3.0f;
+
 FlatScene flatten_scene(const ObjectPtr& top) {
     Flattener f;
     f.run(top.get());
     map_exact_refs(f.out);
+    if (!f.out.wexact.empty()) {
+        // several instance chains (or the top level and a chain): a tree of its own for the
+        // exact kernel, with heavier primitives (smaller leaves)
+        int32_t first = f.out.wexact[0].inst;
+        bool several = false;
+        for (const DExactRef& r : f.out.wexact) several |= r.inst != first;
+        if (several) {
+            std::vector<float> cost = f.wcost;
+            for (float& c : cost) c *= EXACT_SAH_PRIM_COST;
+            try {
+                f.out.wbvh_x = build_world_bvh(f.wbounds, cost);
+                map_exact_refs(f.out);
+            } catch (const std::runtime_error&) {
+                f.out.wbvh_x = WorldBvh();
+                map_exact_refs(f.out);
+            }
+        }
+    }
     return std::move(f.out);
 }
 

@@ -39,9 +39,16 @@ struct FlatScene {
     WorldBvh wbvh;
     std::vector<DPrimWorld<double>> wbvh_prims;  // BVH leaf order
     bool wbvh_ok = false;
-    // Exact reference of each BVH slot (device_scene.hpp DExactRef), when every world
-    // primitive maps onto the exact tree's depth-first walk (instances not nested).
+    // Exact kernel's world-BVH mode: the tree it culls with and the exact reference of each of
+    // its slots (device_scene.hpp DExactRef), when every world primitive maps onto the exact
+    // tree's depth-first walk (instances not nested).  Scenes whose primitives sit under
+    // several instance chains get a tree of their own built with the primitive weight
+    // EXACT_SAH_PRIM_COST (an exact test, and the instance switch before it, cost several
+    // node visits: Cornell 244 -> 226 ms); otherwise wbvh_x stays empty and wbvh is shared.
+    WorldBvh wbvh_x;
     std::vector<DExactRef> wexact;
+    std::vector<uint32_t> wprims_kind;  // kind of each world primitive (depth-first rank)
+    const WorldBvh& exact_tree() const { return wbvh_x.order.empty() ? wbvh : wbvh_x; }
 };
 
 FlatScene flatten_scene(const ObjectPtr& top_level_bvh);

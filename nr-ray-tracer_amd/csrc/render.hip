@@ -125,15 +125,25 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                        nt = (uint32_t)fs.textures.size();
         // f64 view: the exact node array (reference node for node); f32 view: the
         // list-collapsed array with composed instance transforms.
-        // the exact kernel's world-BVH mode culls with the f32 world BVH (same device arrays)
+        const uint32_t wstack = std::max<uint32_t>(1u, use_wbvh4(fs) ? fs.wbvh.stack4 : fs.wbvh.depth);
+        // the exact kernel's world-BVH mode culls with the f32 world BVH, or with a tree of its own
+        // (FlatScene::wbvh_x) on scenes with several instance chains
         auto* wx = (DExactRef*)track(upload(fs.wexact, "wexact"), fs.wexact.size() * sizeof(DExactRef));
         const bool wx_ok = !fs.wexact.empty();
-        const uint32_t wstack = std::max<uint32_t>(1u, use_wbvh4(fs) ? fs.wbvh.stack4 : fs.wbvh.depth);
+        const WorldBvh& xt = fs.exact_tree();
+        const DBvhNode* xbn = wbn;
+        const DBvh4Node* xb4 = wb4;
+        if (&xt != &fs.wbvh) {
+            xbn = (DBvhNode*)track(upload(xt.nodes, "wbvh_x"), xt.nodes.size() * sizeof(DBvhNode));
+            xb4 = (DBvh4Node*)track(upload(xt.nodes4, "wbvh4_x"), xt.nodes4.size() * sizeof(DBvh4Node));
+        }
+        const bool x4 = !xt.nodes4.empty() && use_wbvh4(fs);
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
-                                     nullptr, 0, nullptr, 0, 0, wx_ok ? wbn : nullptr,
-                                     (wx_ok && use_wbvh4(fs)) ? wb4 : nullptr, fs.wbvh.root4, fs.wbvh.root,
-                                     wx_ok ? (uint32_t)fs.wbvh.nodes.size() : 0u, wstack, wx_ok ? wx : nullptr};
+                                     nullptr, 0, nullptr, 0, 0, wx_ok ? xbn : nullptr,
+                                     (wx_ok && x4) ? xb4 : nullptr, xt.root4, xt.root,
+                                     wx_ok ? (uint32_t)xt.nodes.size() : 0u,
+                                     std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? wx : nullptr};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
