@@ -6,9 +6,11 @@ Tolerances (stated):
     operation order; only the radiance product is accumulated forward instead
     of recursively.  So output pixels equal the oracle's to within 1e-12
     relative, and >= 99.9 % are bit-identical after the f32 cast.
-  * f32 + ChaCha8 / Philox: statistical — per-channel image mean within 2 %
-    (small renders) and a per-pixel z-score test against the oracle's
-    per-pixel variance estimate.
+  * f32 + ChaCha8 / Philox: SURVEY §8(d)'s stated tolerance (per-channel mean
+    within 0.5 %, chi^2/N of per-pixel z in [0.9, 1.1]) is checked against
+    high-spp oracle fixtures in tests/test_stat_parity.py; this file adds a
+    coarse screen over more scenes at low spp (image means within 4.5 standard
+    errors, block z-scores) and the same-path check on the ChaCha8 stream.
 """
 import os
 import tempfile
@@ -134,9 +136,11 @@ STAT_CASES = [("scenes/cornell-box-scene.json", 48, 48, 64), ("scenes/spheres.to
                                                  ("f64", "philox", "auto"), ("f32", "philox", "bvh")])
 @pytest.mark.parametrize("case", STAT_CASES, ids=[c[0] for c in STAT_CASES])
 def test_fast_variants_statistically_match(precision, rng, trace, case):
-    """Statistical parity: image means within 4.5 standard errors,
-    per-pixel z-scores (std from the oracle's per-sample variance) with mean
-    z^2 in [0.5, 2] and < 1 % of pixels beyond |z| > 6."""
+    """Coarse statistical screen over six scenes at low spp (the stated tolerance is
+    tests/test_stat_parity.py): per-channel image means within 4.5 standard errors of
+    the oracle's at the same spp; Philox: 4x4-block z-scores with median |z| in
+    [0.35, 1.1] and < 3 % beyond |z| > 5; ChaCha8 (the reference stream): at least
+    half (Cornell) or a quarter of the pixels follow the oracle's paths closely."""
     scene, w, h, spp = case
     with tempfile.TemporaryDirectory() as td:
         tree, _ = oracle_tree(scene, td, width=w, height=h, spp=spp)
