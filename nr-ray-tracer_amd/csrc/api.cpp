@@ -239,6 +239,9 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
             throw std::invalid_argument("Philox mode: image width and height must be < 65536");
         if ((uint64_t)128 * p.spp >= 0xFFFFFFFFull)
             throw std::invalid_argument("samples_per_pixel too large for the Philox sample pool (< 2^25)");
+        if (o->precision == NRT_PRECISION_F32 && (p.spp > PHILOX2_MAX_SPP || p.max_bounces > PHILOX2_MAX_BOUNCES))
+            throw std::invalid_argument("f32 Philox mode: samples_per_pixel <= 2^24 and ray_max_bounces <= 254 "
+                                        "(Philox2x32 counter (pixel, sample | step << 24))");
     }
     // Radiance grid 2^-k: a sample's radiance is at most max(background, emission) x
     // albedo^bounces; k keeps spp such values below 2^52, so the pixel sums are exact
@@ -633,7 +636,9 @@ int nrt_debug_perlin_permutation(uint32_t seed, uint8_t* out) {
 int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out) {
     return guarded(NRT_E_DEVICE, [&]() {
         if (!out && lanes && count) throw std::invalid_argument("null output");
-        if (rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
+        if (rng > RNG_PHILOX2_BLOCK) throw std::invalid_argument("unknown rng");
+        if (rng == RNG_PHILOX2_BLOCK && (count > PHILOX2_STEPS || stream0 + lanes > 0xFFFFFFFFull || sample >= PHILOX2_MAX_SPP))
+            throw std::invalid_argument("Philox2x32 block probe: step, pixel or sample out of range");
         gpu_rng_probe(rng, stream0, lanes, count, sample, out);
         return NRT_OK;
     });

@@ -62,6 +62,8 @@ template <typename R> __device__ __forceinline__ V<R> cross(V<R> a, V<R> b) {
 // hardware reciprocal / reciprocal-sqrt (1 ulp), the f64 kernel IEEE division.
 template <typename R> __device__ __forceinline__ R fast_rcp(R x) { return R(1) / x; }
 template <> __device__ __forceinline__ float fast_rcp<float>(float x) { return __builtin_amdgcn_rcpf(x); }
+template <typename R> __device__ __forceinline__ R fast_sqrt(R x) { return sqrt(x); }
+template <> __device__ __forceinline__ float fast_sqrt<float>(float x) { return __builtin_amdgcn_sqrtf(x); }
 template <typename R> __device__ __forceinline__ R fast_div(R a, R b) { return a / b; }
 template <> __device__ __forceinline__ float fast_div<float>(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 template <typename R> __device__ __forceinline__ V<R> vdiv(V<R> a, R s) { return a / s; }
@@ -236,6 +238,38 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+// Philox2x32-10 (Random123), key 0: one widening multiply and one three-way xor per
+// round, half the work of 4x32.  The f32 render loop needs at most three draws per
+// path segment, which 64 bits cover (Philox::block_at).
+__device__ __forceinline__ uint2 philox2x32_10(uint32_t c0, uint32_t c1) {
+#if NRT_PHILOX_SKEY
+    uint32_t k;
+    asm volatile("s_mov_b32 %0, 0x9e3779b9" : "=s"(k));
+#else
+    uint32_t k = 0u;
+#endif
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p = (uint64_t)0xD256D193u * c0;
+        const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
+        uint32_t n;
+#if NRT_PHILOX_SKEY
+        if (r == 0) {  // key 0
+            n = hi ^ c1;
+        } else {
+            if (r > 1) asm volatile("s_add_u32 %0, %0, 0x9e3779b9" : "+s"(k) : : "scc");
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n) : "v"(hi), "v"(c1), "s"(k));
+        }
+#else
+        if (r > 0) k += 0x9E3779B9u;
+        n = hi ^ c1 ^ k;
+#endif
+        c0 = n;
+        c1 = lo;
+    }
+    return make_uint2(c0, c1);
+}
+
 struct Philox {
     static constexpr bool uses_lds = false;
     static constexpr bool exact_stream = false;  // only the distributions matter
@@ -270,16 +304,27 @@ struct Philox {
         const uint32_t lo = next32();
         return (uint64_t)lo | ((uint64_t)next32() << 32);
     }
-    // Render loop: one whole block per lane per iteration, counter
-    // (pixel, sample, step): step 0 = camera ray, b + 1 = scatter at bounce b.
-    __device__ __forceinline__ uint4 block(uint32_t smp, uint32_t step) const { return block_at(pix, smp, step); }
+    // Render loop: one whole block per lane per iteration, keyed by (pixel, sample,
+    // step): step 0 = camera ray, b + 1 = scatter at bounce b, defocus_step() = the
+    // camera's second block when the defocus disk is on.  The draws are w.x, w.y, w.z.
+    //   f64: Philox4x32-10, counter (pixel, sample, step, 0); 32-bit draws.
+    //   f32: Philox2x32-10, counter (pixel, sample | step << 24) (host: spp <= 2^24,
+    //        bounces <= 254); w.x = lo and w.y = hi (u01 reads their top 23 bits),
+    //        w.z = their low 9 bits each (18-bit draw): disjoint bits of one block.
+    template <typename R>
     static __device__ __forceinline__ uint4 block_at(uint32_t pixel, uint32_t smp, uint32_t step) {
-        uint32_t w[4];
-        philox4x32_10(pixel, smp, step, 0u, w);
-        return make_uint4(w[0], w[1], w[2], w[3]);
+        if constexpr (sizeof(R) == 4) {
+            const uint2 v = philox2x32_10(pixel, smp | (step << 24));
+            return make_uint4(v.x, v.y, (v.x << 23) | ((v.y & 0x1FFu) << 14), 0u);
+        } else {
+            uint32_t w[4];
+            philox4x32_10(pixel, smp, step, 0u, w);
+            return make_uint4(w[0], w[1], w[2], w[3]);
+        }
     }
+    template <typename R>
+    static constexpr uint32_t defocus_step() { return sizeof(R) == 4 ? PHILOX2_STEPS - 1u : 0xFFFFFFFFu; }
 };
-constexpr uint32_t PHILOX_STEP_DEFOCUS = 0xFFFFFFFFu;  // second camera block when the defocus disk is on
 
 // 32-bit word -> uniform [0, 1) (f32: 23 bits, f64: 32 bits)
 template <typename R> __device__ __forceinline__ R u01(uint32_t w);
@@ -347,7 +392,7 @@ template <typename R> __device__ __forceinline__ V<R> unit_ball_inverse(uint32_t
     const R z = R(2) * u01<R>(w0) - R(1);
     const R turn = u01<R>(w1);
     const R w = R(1) - u01<R>(w2);  // (0, 1]
-    const R s = sqrt(fmax(R(0), R(1) - z * z));
+    const R s = fast_sqrt(fmax(R(0), R(1) - z * z));  // f32: v_sqrt_f32 (1 ulp)
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_exp2f(-0.333333343f * __builtin_amdgcn_logf(w));
         const float c = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn);  // argument in turns
@@ -1504,12 +1549,12 @@ template <typename R> __device__ __forceinline__ V<R> reflect(V<R> v, V<R> n) {
 template <typename R> __device__ __forceinline__ V<R> refract(V<R> i, V<R> n, R eta) {
     const R ndi = dot(n, i);
     const R k = R(1.0) - eta * eta * (R(1.0) - ndi * ndi);
-    if (k >= R(0)) return (eta * i) - ((eta * ndi + sqrt(k)) * n);
+    if (k >= R(0)) return (eta * i) - ((eta * ndi + fast_sqrt(k)) * n);
     return mk(R(0), R(0), R(0));
 }
 // dielectric.rs:13-19 (powi(5) = x * ((x*x)*(x*x)))
 template <typename R> __device__ __forceinline__ R reflectance(R cosine, R ri) {
-    R r0 = (R(1.0) - ri) / (R(1.0) + ri);
+    R r0 = fast_div(R(1.0) - ri, R(1.0) + ri);
     r0 = r0 * r0;
     const R x = R(1.0) - cosine;
     const R x2 = x * x;
@@ -1746,10 +1791,10 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         V<R> att = mk(R(1), R(1), R(1));
         bool scattered = true;
         if (m.kind == MAT_DIELECTRIC) {
-            const R ri = h.front ? R(1.0) / m.param : m.param;
+            const R ri = h.front ? fast_div(R(1.0), m.param) : m.param;
             const V<R> unit = normalize(ray.d);
             const R cos_theta = fmin(dot(-unit, h.n), R(1.0));
-            const R sin_theta = sqrt(R(1.0) - cos_theta * cos_theta);
+            const R sin_theta = fast_sqrt(R(1.0) - cos_theta * cos_theta);
             bool refl = ri * sin_theta > R(1.0);
             if (!refl) {
                 R r;
@@ -2017,7 +2062,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
             const V<R> point = (cam(0) + ((R)px + ox) * cam(1)) + ((R)py + oy) * cam(2);
             if (p.defocus) {
-                const uint4 wd = g.block_at(pixel_index(), cur, PHILOX_STEP_DEFOCUS);
+                const uint4 wd = G::template block_at<R>(pixel_index(), cur, G::template defocus_step<R>());
                 const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
                 ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
             } else {
@@ -2137,7 +2182,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
             // this segment's block: the scatter's (pixel, sample, bounce + 1) or the
             // claimed sample's camera block (pixel', sample', 0)
-            w = g.block_at(pixel_index(), cur, scatter ? b + 1u : 0u);
+            w = G::template block_at<R>(pixel_index(), cur, scatter ? b + 1u : 0u);
             const unsigned long long t3 = stamp();
             if (scatter && !scatter_ray(h)) killed = true;
             if (want && alive) {
@@ -2173,6 +2218,17 @@ __global__ void __launch_bounds__(BLOCK) rng_probe_kernel(uint64_t stream0, uint
     g.init(stream, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);
     g.start_sample(sample);
     for (uint32_t k = 0; k < count; ++k) out[(uint64_t)threadIdx.x * count + k] = g.next();
+}
+
+// The f32 render loop's Philox2x32-10 blocks (tests only): lane l, word k = block
+// (pixel0 + l, sample, step k) as lo | hi << 32.
+template <typename R = float>  // (a template: the header is in two translation units)
+__global__ void __launch_bounds__(BLOCK) philox_block_probe_kernel(uint32_t pixel0, uint32_t count, uint32_t sample,
+                                                                   unsigned long long* out) {
+    for (uint32_t k = 0; k < count; ++k) {
+        const uint4 w = Philox::block_at<R>(pixel0 + threadIdx.x, sample, k);
+        out[(uint64_t)threadIdx.x * count + k] = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
+    }
 }
 
 }  // namespace dev

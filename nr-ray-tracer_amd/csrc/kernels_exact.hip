@@ -23,8 +23,11 @@ void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t c
     if (rng == RNG_CHACHA8)
         hipLaunchKernelGGL(dev::rng_probe_kernel<dev::ChaCha8>, dim3(1), dim3(lanes),
                            dev::RING * dev::BLOCK * sizeof(uint2), 0, stream0, count, sample, d);
-    else
+    else if (rng == RNG_PHILOX)
         hipLaunchKernelGGL(dev::rng_probe_kernel<dev::Philox>, dim3(1), dim3(lanes), 0, 0, stream0, count, sample, d);
+    else  // RNG_PHILOX2_BLOCK: the f32 render loop's blocks, word k = step k
+        hipLaunchKernelGGL(dev::philox_block_probe_kernel<float>, dim3(1), dim3(lanes), 0, 0, (uint32_t)stream0, count,
+                           sample, d);
 }
 
 }  // namespace nrt

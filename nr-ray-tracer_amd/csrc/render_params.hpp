@@ -9,7 +9,11 @@ constexpr uint32_t QUEUE_HEADS = 8;    // one per XCD
 constexpr uint32_t QUEUE_STRIDE = 32;  // words: one 128-B line per head
 
 
-enum : uint32_t { RNG_CHACHA8 = 0, RNG_PHILOX = 1 };
+enum : uint32_t { RNG_CHACHA8 = 0, RNG_PHILOX = 1, RNG_PHILOX2_BLOCK = 2 /* nrt_debug_rng only */ };
+// f32 Philox render loop: Philox2x32-10 counter (pixel, sample | step << 24), so
+// spp <= 2^24 and steps 0..255 (camera 0, scatters 1..max_bounces, defocus 255).
+constexpr uint32_t PHILOX2_STEPS = 256, PHILOX2_MAX_SPP = 1u << 24;
+constexpr uint32_t PHILOX2_MAX_BOUNCES = PHILOX2_STEPS - 2u;
 
 struct RenderParams {
     // Camera after CameraBuilder::build (camera.rs:205-227), always f64 on the host.

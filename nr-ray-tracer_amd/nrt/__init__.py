@@ -508,9 +508,13 @@ def to_rgb8(img: np.ndarray, gamma: float = 0.5) -> np.ndarray:
 
 
 def debug_rng(rng: str, stream0: int, lanes: int, count: int, sample: int = 0) -> np.ndarray:
-    """First `count` draws of `lanes` consecutive pixel streams, computed on the GPU."""
+    """First `count` draws of `lanes` consecutive pixel streams, computed on the GPU.
+
+    rng "philox2x32_block": the f32 render loop's Philox2x32-10 blocks instead, word k of
+    lane l = block (pixel stream0 + l, `sample`, step k) as lo | hi << 32 (nrt.h)."""
+    code = 2 if rng == "philox2x32_block" else RNG[rng]
     out = np.empty((lanes, count), dtype=np.uint64)
-    _check(lib().nrt_debug_rng(RNG[rng], stream0, lanes, count, sample, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+    _check(lib().nrt_debug_rng(code, stream0, lanes, count, sample, out.ctypes.data_as(C.POINTER(C.c_uint64))))
     return out
 
 

@@ -72,6 +72,20 @@ def test_philox_kat():
     assert w == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
 
 
+@pytest.mark.parametrize("pixel0,sample", [(0, 0), (1000, 5), (2 ** 21 - 64, 2 ** 24 - 1)])
+def test_philox2x32_render_blocks(pixel0, sample):
+    # the f32 render loop's blocks (kernel.hpp Philox::block_at<float>): Philox2x32-10 of
+    # counter (pixel, sample | step << 24), key 0 -- Random123's zero KAT at (0, 0, 0)
+    from test_oracle import py_philox2x32_10
+    got = nrt.debug_rng("philox2x32_block", pixel0, 64, 256, sample=sample)
+    if pixel0 == 0 and sample == 0:
+        assert int(got[0, 0]) == 0x6CD10DF2FF1DAE59
+    for lane in (0, 1, 31, 63):
+        for step in (0, 1, 2, 50, 254, 255):
+            lo, hi = py_philox2x32_10(pixel0 + lane, sample | (step << 24))
+            assert int(got[lane, step]) == lo | (hi << 32), (lane, step)
+
+
 @pytest.mark.parametrize("scene,w,h,spp,bounces", CASES_F64)
 def test_f64_chacha8_matches_oracle(scene, w, h, spp, bounces):
     want = reference(scene, w, h, spp, bounces)

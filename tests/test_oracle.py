@@ -137,3 +137,24 @@ def test_pixel_stream(stream):
     r = subprocess.run([ORACLE_BIN, "rng", str(stream), "80"], check=True, capture_output=True, text=True)
     got = [int(x, 16) for x in r.stdout.split()]
     assert got == py_stream(stream, 80)
+
+
+def py_philox2x32_10(c0, c1, key=0):
+    """Philox2x32-10 (Salmon et al., SC'11; Random123 philox.h): the f32 render loop's RNG
+    (kernel.hpp philox2x32_10, key 0).  Round: (hi, lo) = 0xD256D193 * c0,
+    (c0, c1) = (hi ^ key ^ c1, lo); key += 0x9E3779B9 between rounds."""
+    for _ in range(10):
+        p = 0xD256D193 * c0
+        c0, c1 = (p >> 32) ^ key ^ c1, p & 0xFFFFFFFF
+        key = (key + 0x9E3779B9) & 0xFFFFFFFF
+    return c0, c1
+
+
+@pytest.mark.parametrize("ctr,key,want", [
+    ((0x00000000, 0x00000000), 0x00000000, (0xff1dae59, 0x6cd10df2)),
+    ((0xffffffff, 0xffffffff), 0xffffffff, (0x2c3f628b, 0xab4fd7ad)),
+    ((0x243f6a88, 0x85a308d3), 0x13198a2e, (0xdd7ce038, 0xf62a4c12)),
+])
+def test_philox2x32_random123_kat(ctr, key, want):
+    # Random123 kat_vectors, philox2x32 10 rounds
+    assert py_philox2x32_10(*ctr, key) == want
