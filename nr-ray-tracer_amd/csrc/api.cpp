@@ -221,6 +221,9 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     if (const char* e = std::getenv("NRT_EXACT_ALL")) p.exact_all = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.exact_wbvh = (!p.exact_all && mode == NRT_EXACT_WORLD) ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_WBVH")) p.exact_wbvh = std::strtol(e, nullptr, 10) != 0 && !f.wexact.empty();
+    // (plane-only scenes: the exact world mode's f32 prefilter; knob NRT_EXACT_PF=0 turns it off)
+    p.exact_pf = 1;
+    if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;

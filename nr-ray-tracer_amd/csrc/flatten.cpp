@@ -1064,6 +1064,7 @@ float round_up(double x) {
 // any disagreement in count or kind, leave the mapping empty (mode unavailable).
 static void map_exact_refs(FlatScene& s) {
     s.wexact.clear();
+    s.wexact_prims.clear();
     const WorldBvh& tree = s.exact_tree();
     if (!s.wbvh_ok || tree.order.empty()) return;
     std::vector<std::pair<uint32_t, int32_t>> seq;
@@ -1104,7 +1105,13 @@ static void map_exact_refs(FlatScene& s) {
         if (e.first >= s.prims.size() || s.prims[e.first].kind != wkind) return;
         refs[slot] = DExactRef{e.first, e.second, rank, 0u};
     }
+    // the same slots' world primitives (the shared tree's slot order is wbvh.order)
+    std::vector<uint32_t> shared_slot(s.wbvh.order.size());
+    for (size_t k = 0; k < s.wbvh.order.size(); ++k) shared_slot[s.wbvh.order[k]] = (uint32_t)k;
+    std::vector<DPrimWorld<double>> prims(tree.order.size());
+    for (size_t slot = 0; slot < prims.size(); ++slot) prims[slot] = s.wbvh_prims[shared_slot[tree.order[slot]]];
     s.wexact = std::move(refs);
+    s.wexact_prims = std::move(prims);
 }
 
 constexpr float EXACT_SAH_PRIM_COST = 3.0f;
@@ -1166,6 +1173,7 @@ FlatScene32 to_f32(const FlatScene& s) {
     };
     world32(s.wprims, o.wprims);
     world32(s.wbvh_prims, o.wbvh_prims);
+    world32(s.wexact_prims, o.wexact_prims);
     o.inst_fast.resize(s.inst_fast.size());
     for (size_t i = 0; i < s.inst_fast.size(); ++i) {
         const auto& a = s.inst_fast[i];

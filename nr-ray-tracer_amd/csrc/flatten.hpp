@@ -47,6 +47,7 @@ struct FlatScene {
     // node visits: Cornell 244 -> 226 ms); otherwise wbvh_x stays empty and wbvh is shared.
     WorldBvh wbvh_x;
     std::vector<DExactRef> wexact;
+    std::vector<DPrimWorld<double>> wexact_prims;  // world primitive of each exact-tree slot (prefilter)
     std::vector<uint32_t> wprims_kind;  // kind of each world primitive (depth-first rank)
     const WorldBvh& exact_tree() const { return wbvh_x.order.empty() ? wbvh : wbvh_x; }
 };
@@ -63,6 +64,7 @@ struct FlatScene32 {
     std::vector<DPrimFast<float>> fprims;
     std::vector<DPrimWorld<float>> wprims;
     std::vector<DPrimWorld<float>> wbvh_prims;
+    std::vector<DPrimWorld<float>> wexact_prims;
 };
 FlatScene32 to_f32(const FlatScene& s);
 

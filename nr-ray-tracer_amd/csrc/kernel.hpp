@@ -1308,12 +1308,157 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
     return best_prim >= 0;
 }
 
-template <typename R, int MAXD, bool EXACT, bool FLAT = false>
+// Exact world mode with an f32 prefilter (plane-only scenes, RenderParams::exact_pf).
+// Phase 1 traverses the same tree in f32 and tests each reached primitive's world-space copy
+// (wxprims) in f32 with a forward error bound on t, alpha and beta, relative to the magnitudes
+// that enter them (absolute dot products; E = 2^-17 is 64x the f32 unit roundoff, which covers
+// the f32 rounding of the flattened coefficients and of the ray, the f32 arithmetic and the
+// reference's f64 rounding, for scale factors well below 2^20).  A primitive is
+//   a certain miss   when the bounds put it outside Plane::hit's acceptance (|n.d| < 1e-8,
+//                    t < 0.001, alpha / beta outside the quad or triangle): dropped;
+//   a certain hit    when they put it inside: its upper bound t_hi bounds the winner's exact t;
+//   a candidate      otherwise, kept while its lower bound t_lo <= the smallest t_hi so far.
+// The winner (the reference's closest hit, plane.rs:141-174, object.rs:89-121) is accepted by
+// the reference tests and its exact t is <= every certain hit's, so it is a candidate whose
+// t_lo survives; phase 2 runs the reference tests in f64 on the surviving candidates only
+// (smallest exact t, ties to the higher depth-first rank, as trace_exact_wbvh).  Boxes are cut
+// at the bound raised by 2^-20 as there.  A lane with more than XCAND live candidates at once
+// (never seen on the reference scenes) falls back to trace_exact_wbvh.
+constexpr int XCAND = 4;
+__device__ __forceinline__ float absdot(V<float> a, V<float> b) {
+    return fabsf(a.x * b.x) + fabsf(a.y * b.y) + fabsf(a.z * b.z);
+}
+// false: certain miss; otherwise [tlo, thi] bounds the reference's t and `certain` is set
+// when the reference test surely accepts the primitive
+__device__ __forceinline__ bool exact_prefilter(const DPrimWorld<float>& q, const Ray<float>& r, float& tlo,
+                                                float& thi, bool& certain) {
+    constexpr float E = 0x1p-17f;
+    const V<float> N = ld3(q.N);
+    const float den = dot(N, r.d), aden = fabsf(den), eden = E * absdot(N, r.d);
+    certain = false;
+    tlo = -INFINITY;
+    thi = INFINITY;
+    if (aden + eden < 1e-8f) return false;           // |n.d| < 1e-8: the reference rejects it
+    if (!(aden - 2.0f * eden > 1e-8f)) return true;  // near-parallel (or NaN): a candidate
+    const float t = (q.D - dot(N, r.o)) / den;
+    const float at = fabsf(t);
+    const float et = (E * (fabsf(q.D) + absdot(N, r.o)) + at * eden) / (aden - eden) + E * at;
+    if (t + et < 0.001f) return false;  // t < 0.001
+    const V<float> P = mk(fabsf(r.o.x) + at * fabsf(r.d.x), fabsf(r.o.y) + at * fabsf(r.d.y),
+                          fabsf(r.o.z) + at * fabsf(r.d.z));  // bounds |o + t d| per axis
+    const V<float> p = r.o + t * r.d;
+    const V<float> A = mk(q.AB[0], q.AB[2], q.AB[4]), B = mk(q.AB[1], q.AB[3], q.AB[5]);
+    const float al = dot(p, A) - q.AB[6], be = dot(p, B) - q.AB[7];
+    const float ea = E * (absdot(A, P) + fabsf(q.AB[6])) + et * absdot(A, r.d);
+    const float eb = E * (absdot(B, P) + fabsf(q.AB[7])) + et * absdot(B, r.d);
+    bool miss, in;
+    if ((q.meta & WKIND_MASK) == PRIM_QUAD) {  // closed [0, 1]^2
+        miss = (al + ea < 0.0f) | (al - ea > 1.0f) | (be + eb < 0.0f) | (be - eb > 1.0f);
+        in = (al - ea >= 0.0f) & (al + ea <= 1.0f) & (be - eb >= 0.0f) & (be + eb <= 1.0f);
+    } else {  // triangle, open
+        miss = (al + ea <= 0.0f) | (be + eb <= 0.0f) | (al + be - (ea + eb) >= 1.0f);
+        in = (al - ea > 0.0f) & (be - eb > 0.0f) & (al + be + (ea + eb) < 1.0f);
+    }
+    if (miss) return false;
+    tlo = t - et;
+    thi = t + et;
+    certain = in & (tlo >= 0.001f) & (thi < INFINITY);
+    if (!(tlo == tlo)) tlo = -INFINITY;  // NaN bound: keep the candidate
+    if (!(thi == thi)) thi = INFINITY;
+    return true;
+}
+
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
+    Ray<float> fr;
+    fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    WbvhTrav ts;
+    wbvh_begin(ts, wbvh_root(sc), fr);
+    float bound = INFINITY;  // smallest t_hi of a certain hit so far
+    int32_t cs[XCAND];       // candidate slots (-1: free) and their t_lo
+    float cl[XCAND];
+#pragma unroll
+    for (int j = 0; j < XCAND; ++j) {
+        cs[j] = -1;
+        cl[j] = INFINITY;
+    }
+    bool over = false;
+    {
+        PrivStack stk;
+        while (true) {
+            while (ts.node >= 0) {
+                if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
+                else wbvh2_visit<R>(ts, sc, stk);
+            }
+            if (ts.node == WBVH_DONE) break;
+            const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const DPrimWorld<float> q = load16(sc.wxprims + first + k);
+                float tlo, thi;
+                bool certain;
+                if (!exact_prefilter(q, fr, tlo, thi, certain) || tlo > bound) continue;
+                if (certain && thi < bound) {
+                    bound = thi;
+                    ts.t_best = bound * (1.0f + 0x1p-20f);
+                }
+                // the first free slot, or one whose lower bound the bound has passed
+                bool placed = false;
+#pragma unroll
+                for (int j = 0; j < XCAND; ++j) {
+                    const bool here = !placed && (cs[j] < 0 || cl[j] > bound);
+                    cs[j] = here ? (int32_t)(first + k) : cs[j];
+                    cl[j] = here ? tlo : cl[j];
+                    placed |= here;
+                }
+                over |= !placed;
+            }
+            ts.node = wbvh_pop(ts, stk);
+        }
+    }
+    if (over) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+    // phase 2: the reference tests on the surviving candidates
+    R best_t = R(INFINITY);
+    uint32_t best_rank = 0;
+    int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
+    Ray<R> oray = wray;
+#pragma unroll
+    for (int j = 0; j < XCAND; ++j) {
+        if (cs[j] >= 0 && cl[j] <= bound) {
+            const DExactRef ref = sc.wexact[cs[j]];
+            if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
+                oray = wray;
+                if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
+                cur_inst = ref.inst;
+            }
+            R alpha, beta;
+            V<R> point;
+            const R t = plane_t(sc.prims[ref.prim], oray, alpha, beta, point);
+            if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
+                best_t = t;
+                best_rank = ref.rank;
+                best_prim = (int32_t)ref.prim;
+                best_inst = ref.inst;
+            }
+        }
+    }
+    hm.t = best_t;
+    hm.prim = (uint32_t)best_prim;
+    hm.depth = best_inst >= 0 ? 1 : 0;
+    hm.inst[0] = (uint32_t)best_inst;
+    return best_prim >= 0;
+}
+
+template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                      int32_t* stack, bool all = false, bool exact_wbvh = false) {
+                                      int32_t* stack, bool all = false, bool exact_wbvh = false, bool pf = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
+        if constexpr (PF) {  // plane-only scenes (KF_PLANES)
+            if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm);
+        }
         if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
         return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
     } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
@@ -1937,8 +2082,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
-                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0,
-                                                      p.exact_wbvh != 0);
+                    hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0>(
+                        MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf != 0);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);

@@ -56,6 +56,9 @@ struct RenderParams {
     // (DSceneView::wexact): the f32 world BVH culls, the reference tests decide (kernel.hpp
     // trace_exact_wbvh).
     uint32_t exact_wbvh;
+    // Exact world mode, plane-only scenes (KF_PLANES): an f32 prefilter with error bounds picks
+    // the candidates, and only those get the reference tests (kernel.hpp trace_exact_wbvh_pf).
+    uint32_t exact_pf;
 };
 
 }  // namespace nrt

@@ -86,6 +86,16 @@ def test_philox2x32_render_blocks(pixel0, sample):
             assert int(got[lane, step]) == lo | (hi << 32), (lane, step)
 
 
+def test_f32_philox_counter_limits():
+    # the Philox2x32 counter holds the sample in 24 bits and the path step in 8 (nrt.h)
+    with pytest.raises(nrt.NrtError):
+        load("scenes/cornell-box-scene.json", 1, 1, 2 ** 24 + 1).render(precision="f32", rng="philox")
+    with pytest.raises(nrt.NrtError):
+        load("scenes/cornell-box-scene.json", 1, 1, 1, 255).render(precision="f32", rng="philox")
+    img = load("scenes/cornell-box-scene.json", 2, 2, 1, 254).render(precision="f32", rng="philox")
+    assert np.isfinite(img).all()
+
+
 @pytest.mark.parametrize("scene,w,h,spp,bounces", CASES_F64)
 def test_f64_chacha8_matches_oracle(scene, w, h, spp, bounces):
     want = reference(scene, w, h, spp, bounces)
@@ -243,16 +253,19 @@ def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
 ])
 def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     """The three traversals of the reference-exact kernel (nrt.h nrt_exact_mode: the reference
-    tree, every primitive in depth-first order, f32 world-BVH culling with the reference tests)
-    find the same closest hit with the same tie-break, so the f64/ChaCha8 frames are equal bit
-    for bit (BVH::hit, object.rs:89-121)."""
+    tree, every primitive in depth-first order, f32 world-BVH culling with the reference tests,
+    the last with and without the f32 prefilter of plane-only scenes, kernel.hpp
+    trace_exact_wbvh_pf) find the same closest hit with the same tie-break, so the f64/ChaCha8
+    frames are equal bit for bit (BVH::hit, object.rs:89-121)."""
     s = load(scene, w, h, spp)
     frames = {}
-    for name, env in {"bvh": ("0", "0"), "all": ("1", "0"), "world": ("0", "1")}.items():
-        if name == "world" and s.stats()["exact_mode"] != 2:
+    modes = {"bvh": ("0", "0", "0"), "all": ("1", "0", "0"), "world": ("0", "1", "0"), "world_pf": ("0", "1", "1")}
+    for name, env in modes.items():
+        if name.startswith("world") and s.stats()["exact_mode"] != 2:
             continue
         monkeypatch.setenv("NRT_EXACT_ALL", env[0])
         monkeypatch.setenv("NRT_EXACT_WBVH", env[1])
+        monkeypatch.setenv("NRT_EXACT_PF", env[2])
         frames[name] = s.render(precision="f64", rng="chacha8")
     base = frames.pop("bvh")
     assert np.isfinite(base).all()
