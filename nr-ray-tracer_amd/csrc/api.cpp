@@ -221,7 +221,8 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     if (const char* e = std::getenv("NRT_EXACT_ALL")) p.exact_all = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.exact_wbvh = (!p.exact_all && mode == NRT_EXACT_WORLD) ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_WBVH")) p.exact_wbvh = std::strtol(e, nullptr, 10) != 0 && !f.wexact.empty();
-    // (plane-only scenes: the exact world mode's f32 prefilter; knob NRT_EXACT_PF=0 turns it off)
+    // plane-only scenes: the exact world mode's f32 prefilter (knob NRT_EXACT_PF=0 turns it off;
+    // over every slot instead of the walk measured slower on Cornell, 223 against 217 ms)
     p.exact_pf = 1;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;

@@ -280,6 +280,7 @@ struct DSceneView {
     uint32_t wbvh_stack;
     const DExactRef* wexact;  // f64 view: exact reference of each world-BVH slot (exact_wbvh mode)
     const DPrimWorld<float>* wxprims;  // f64 view: f32 world primitive of each of those slots (prefilter)
+    uint32_t n_wexact;                 // slots of that tree
 };
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each

@@ -1368,65 +1368,54 @@ __device__ __forceinline__ bool exact_prefilter(const DPrimWorld<float>& q, cons
     return true;
 }
 
-template <typename R, int MAXD>
-__device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
-    static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
-    Ray<float> fr;
-    fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
-    fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
-    WbvhTrav ts;
-    wbvh_begin(ts, wbvh_root(sc), fr);
-    float bound = INFINITY;  // smallest t_hi of a certain hit so far
-    int32_t cs[XCAND];       // candidate slots (-1: free) and their t_lo
+// Candidate list of the prefilter: slots (-1: free) and their t_lo; a new candidate takes the
+// first free slot or one whose t_lo the bound has passed, else the list overflows.
+struct XCands {
+    int32_t cs[XCAND];
     float cl[XCAND];
+    float bound;  // smallest t_hi of a certain hit so far
+    bool over;
+    __device__ __forceinline__ void init() {
 #pragma unroll
-    for (int j = 0; j < XCAND; ++j) {
-        cs[j] = -1;
-        cl[j] = INFINITY;
-    }
-    bool over = false;
-    {
-        PrivStack stk;
-        while (true) {
-            while (ts.node >= 0) {
-                if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
-                else wbvh2_visit<R>(ts, sc, stk);
-            }
-            if (ts.node == WBVH_DONE) break;
-            const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const DPrimWorld<float> q = load16(sc.wxprims + first + k);
-                float tlo, thi;
-                bool certain;
-                if (!exact_prefilter(q, fr, tlo, thi, certain) || tlo > bound) continue;
-                if (certain && thi < bound) {
-                    bound = thi;
-                    ts.t_best = bound * (1.0f + 0x1p-20f);
-                }
-                // the first free slot, or one whose lower bound the bound has passed
-                bool placed = false;
-#pragma unroll
-                for (int j = 0; j < XCAND; ++j) {
-                    const bool here = !placed && (cs[j] < 0 || cl[j] > bound);
-                    cs[j] = here ? (int32_t)(first + k) : cs[j];
-                    cl[j] = here ? tlo : cl[j];
-                    placed |= here;
-                }
-                over |= !placed;
-            }
-            ts.node = wbvh_pop(ts, stk);
+        for (int j = 0; j < XCAND; ++j) {
+            cs[j] = -1;
+            cl[j] = INFINITY;
         }
+        bound = INFINITY;
+        over = false;
     }
-    if (over) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
-    // phase 2: the reference tests on the surviving candidates
+    // prefilter slot `slot` (world primitive q); true when the bound tightened
+    __device__ __forceinline__ bool offer(const DPrimWorld<float>& q, const Ray<float>& fr, uint32_t slot) {
+        float tlo, thi;
+        bool certain;
+        if (!exact_prefilter(q, fr, tlo, thi, certain) || tlo > bound) return false;
+        const bool tight = certain && thi < bound;
+        bound = tight ? thi : bound;
+        bool placed = false;
+#pragma unroll
+        for (int j = 0; j < XCAND; ++j) {
+            const bool here = !placed && (cs[j] < 0 || cl[j] > bound);
+            cs[j] = here ? (int32_t)slot : cs[j];
+            cl[j] = here ? tlo : cl[j];
+            placed |= here;
+        }
+        over |= !placed;
+        return tight;
+    }
+};
+// Phase 2: the reference tests on the surviving candidates (smallest exact t, ties to the
+// higher depth-first rank, as trace_exact_wbvh).
+template <typename R, int MAXD>
+__device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<R>& sc, const Ray<R>& wray,
+                                              HitMin<R, MAXD>& hm) {
     R best_t = R(INFINITY);
     uint32_t best_rank = 0;
     int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
     Ray<R> oray = wray;
 #pragma unroll
     for (int j = 0; j < XCAND; ++j) {
-        if (cs[j] >= 0 && cl[j] <= bound) {
-            const DExactRef ref = sc.wexact[cs[j]];
+        if (c.cs[j] >= 0 && c.cl[j] <= c.bound) {
+            const DExactRef ref = sc.wexact[c.cs[j]];
             if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
                 oray = wray;
                 if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
@@ -1450,9 +1439,38 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     return best_prim >= 0;
 }
 
+// The prefilter over the world-BVH walk (RenderParams::exact_pf).
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
+    Ray<float> fr;
+    fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    WbvhTrav ts;
+    wbvh_begin(ts, wbvh_root(sc), fr);
+    XCands c;
+    c.init();
+    {
+        PrivStack stk;
+        while (true) {
+            while (ts.node >= 0) {
+                if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
+                else wbvh2_visit<R>(ts, sc, stk);
+            }
+            if (ts.node == WBVH_DONE) break;
+            const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+            for (uint32_t k = 0; k < cnt; ++k)
+                if (c.offer(load16(sc.wxprims + first + k), fr, first + k)) ts.t_best = c.bound * (1.0f + 0x1p-20f);
+            ts.node = wbvh_pop(ts, stk);
+        }
+    }
+    if (c.over) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+    return xcands_finish(c, sc, wray, hm);
+}
+
 template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                      int32_t* stack, bool all = false, bool exact_wbvh = false, bool pf = false) {
+                                      int32_t* stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
@@ -1965,7 +1983,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         tp = tp * att;
         ray.o = h.p;
         ray.d = dir;
-        if constexpr (MAXD > 0) prep_ray<R, EXACT>(ray);  // world modes need no 1/d here
+        if constexpr (MAXD > 0) {  // world modes need no 1/d here, nor the exact kernel's walks
+            if (!EXACT || !(p.exact_all || p.exact_wbvh)) prep_ray<R, EXACT>(ray);
+        }
         bounced = true;
         ++b;
         return true;
@@ -1995,7 +2015,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
-            prep_ray<R, EXACT>(ray);
+            if (!EXACT || !(p.exact_all || p.exact_wbvh)) prep_ray<R, EXACT>(ray);  // 1/d: box tests only
             tp = mk(R(1), R(1), R(1));
             b = 0;
             bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
@@ -2083,7 +2103,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
                     hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0>(
-                        MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf != 0);
+                        MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);

@@ -146,7 +146,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                      (wx_ok && x4) ? xb4 : nullptr, xt.root4, xt.root,
                                      wx_ok ? (uint32_t)xt.nodes.size() : 0u,
                                      std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? wx : nullptr,
-                                     wx_ok ? wxp : nullptr};
+                                     wx_ok ? wxp : nullptr, wx_ok ? (uint32_t)fs.wexact.size() : 0u};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
@@ -154,7 +154,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
                                     (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
                                     fs.wbvh.root4, fs.wbvh.root,
-                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, nullptr};
+                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, nullptr, 0u};
         ds->wbvh_ok = fs.wbvh_ok;
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->planes = !fs.prims.empty();

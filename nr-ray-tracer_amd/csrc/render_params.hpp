@@ -57,7 +57,8 @@ struct RenderParams {
     // trace_exact_wbvh).
     uint32_t exact_wbvh;
     // Exact world mode, plane-only scenes (KF_PLANES): an f32 prefilter with error bounds picks
-    // the candidates, and only those get the reference tests (kernel.hpp trace_exact_wbvh_pf).
+    // the candidates of the world-BVH walk, and only those get the reference tests (kernel.hpp
+    // trace_exact_wbvh_pf).
     uint32_t exact_pf;
 };
 
