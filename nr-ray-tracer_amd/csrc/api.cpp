@@ -272,8 +272,12 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
                     std::log2(alb) * (double)std::min<uint32_t>(p.max_bounces, 8u);
         int k = 50 - (int)std::ceil(std::fmax(lg, -100.0));
         k = std::max(-900, std::min(k, 900));
+        // f32 kernels scale and round in f32 (exact for a power of two in f32 range): the grid
+        // exponent stays in [-126, 127] (only radiance x spp beyond 2^176 or below 2^-77 moves it)
+        if (o && o->precision == NRT_PRECISION_F32) k = std::max(-126, std::min(k, 127));
         p.acc_scale = std::ldexp(1.0, k);
         p.acc_unscale = std::ldexp(1.0, -k);
+        p.acc_scale_f = std::ldexp(1.0f, k);
     }
     p.row_offset = o ? o->row_offset : 0;
     p.row_stride = (o && o->row_stride > 1) ? o->row_stride : 1;

@@ -705,7 +705,9 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
             const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
             const bool entry = tn >= 0.001f;
             const float t = entry ? tn : tf;
-            const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+            // = (tn <= tf) & (t >= 0.001) & (t <= t_best): an entry t is >= 0.001 by choice,
+            // an exit t = tf (tn < 0.001 <= tf then orders the slab)
+            const bool ok = (t <= fminf(tf, t_best)) & (t >= 0.001f);
             const uint32_t sx = ia < 0.0f ? 1u : 0u, sz = ib < 0.0f ? 5u : 4u;
             uint32_t se = sz, sxit = sz ^ 1u;
             se = tn == ny ? entry_slot[1] : se;
@@ -736,7 +738,7 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
             // entry face unless it lies before t_min (origin on or inside the box): then the exit face
             const bool entry = tn >= 0.001f;
             const float t = entry ? tn : tf;
-            const bool ok = (tn <= tf) & (t >= 0.001f) & (t <= t_best);
+            const bool ok = (t <= fminf(tf, t_best)) & (t >= 0.001f);  // (as PRIM_BOXY)
             // face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0),
             // then the quad that lies there (3 bits per slot in meta)
             const uint32_t sx = ix < 0.0f ? 1u : 0u, sy = iy < 0.0f ? 3u : 2u, sz = iz < 0.0f ? 5u : 4u;
@@ -2312,9 +2314,15 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const bool ends = sh && !scatter;
             if (ends && (contrib.x != R(0) || contrib.y != R(0) || contrib.z != R(0))) {
                 double* a = acc + (slot * P + j) * 3u;
-                atomicAdd(a, rint((double)contrib.x * p.acc_scale));
-                atomicAdd(a + 1, rint((double)contrib.y * p.acc_scale));
-                atomicAdd(a + 2, rint((double)contrib.z * p.acc_scale));
+                if constexpr (sizeof(R) == 4) {  // 2^k scaling and rint exact in f32 (host: k in range)
+                    atomicAdd(a, (double)__builtin_rintf(contrib.x * p.acc_scale_f));
+                    atomicAdd(a + 1, (double)__builtin_rintf(contrib.y * p.acc_scale_f));
+                    atomicAdd(a + 2, (double)__builtin_rintf(contrib.z * p.acc_scale_f));
+                } else {
+                    atomicAdd(a, rint((double)contrib.x * p.acc_scale));
+                    atomicAdd(a + 1, rint((double)contrib.y * p.acc_scale));
+                    atomicAdd(a + 2, rint((double)contrib.z * p.acc_scale));
+                }
             }
 #pragma unroll
             for (uint32_t k = 0; k < NS; ++k) dones[k] += (uint32_t)__popcll(__ballot(ends && slot == k));

@@ -60,6 +60,7 @@ struct RenderParams {
     // the candidates of the world-BVH walk, and only those get the reference tests (kernel.hpp
     // trace_exact_wbvh_pf).
     uint32_t exact_pf;
+    float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
 };
 
 }  // namespace nrt
