@@ -363,6 +363,8 @@ def main():
             "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4)},
             "frame_sha256": frame_sha,
             "build_id": nrt.build_id(),  # sha256 prefix of the sources libnrt.so was built from
+            # scene-specialised world-list kernels (jit.hip): built with hiprtc in this process, renders using one
+            "jit": nrt.jit_stats(),
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)

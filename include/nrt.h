@@ -146,6 +146,10 @@ int nrt_abi_version(void);
 /* sha256 prefix of the library's sources it was built from (build provenance; no reference
  * counterpart) */
 const char* nrt_build_id(void);
+/* Scene-specialised world-list kernels (built with hiprtc when a scene is first rendered in
+ * f32 / Philox world-list mode; NRT_JIT=0 turns them off): out[0] = kernels built in this
+ * process, out[1] = renders that used one.  No reference counterpart. */
+int nrt_jit_stats(uint64_t out[2]);
 const char* nrt_last_error(void);   /* thread-local; message text mirrors anyhow's */
 int nrt_device_count(void);
 

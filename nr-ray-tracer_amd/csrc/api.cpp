@@ -315,6 +315,16 @@ int nrt_abi_version(void) { return NRT_ABI_VERSION; }
 #define NRT_SRC_HASH "unknown"
 #endif
 const char* nrt_build_id(void) { return NRT_SRC_HASH; }
+
+int nrt_jit_stats(uint64_t out[2]) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!out) throw std::invalid_argument("null output");
+        const JitCounts c = gpu_jit_counts();
+        out[0] = c.compiled;
+        out[1] = c.launches;
+        return NRT_OK;
+    });
+}
 const char* nrt_last_error(void) { return g_last_error.c_str(); }
 int nrt_device_count(void) { return gpu_device_count(); }
 

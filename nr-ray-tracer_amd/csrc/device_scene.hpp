@@ -19,7 +19,9 @@
 // kernel, float for the fast kernel.  Nothing here is torch-aware.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <cstdint>
+#endif
 
 namespace nrt {
 

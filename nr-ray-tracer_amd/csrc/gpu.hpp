@@ -22,6 +22,10 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
 // f32 kernel mode for nrt_trace `trace`: 0 = world-space list, 1 / MAX_INSTANCE_DEPTH = instance BVH.
 int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace);
 // First `count` draws of `lanes` consecutive streams starting at stream0 (tests).
+struct JitCounts {
+    uint64_t compiled, launches;
+};
+JitCounts gpu_jit_counts();  // scene-specialised kernels (jit.hip)
 void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out);
 
 }  // namespace nrt

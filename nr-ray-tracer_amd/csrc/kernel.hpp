@@ -17,10 +17,12 @@
 //           on the host, every lane tests every primitive (small scenes).
 #pragma once
 
+#ifndef __HIPCC_RTC__  // (hiprtc: the runtime and <cstdint> types are built in, jit.hip)
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
 #include <cstdint>
+#endif
 
 #include "device_scene.hpp"
 #include "render_params.hpp"
@@ -784,7 +786,27 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
     }
 }
 
-template <typename R, int MAXD, bool FLAT = false>
+// World-list signature of a scene-specialised kernel (jit.hip): the run words (kind | count <<
+// WRUN_KIND_BITS, FlatScene::wruns) as template arguments, so the run loop unrolls with each
+// unit's test and scalar loads known at compile time.  NoSig: the generic loop over sc.wruns.
+struct NoSig {
+    static constexpr uint32_t n = 0;
+};
+template <uint32_t... RUNS>
+struct WorldSig {
+    static constexpr uint32_t n = sizeof...(RUNS);
+};
+template <bool FLAT, uint32_t... RUNS>
+__device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float> wp, uint32_t& k, const Ray<float>& ray,
+                                         const f32x2& dox, const f32x2& doy, const f32x2& doz, const float inv[3],
+                                         const float oinv[3], const uint32_t entry_slot[3], float& t_best,
+                                         int32_t& best) {
+    (world_run<FLAT>(wp, RUNS & WRUN_KIND_MASK, k, RUNS >> WRUN_KIND_BITS, ray, dox, doy, doz, inv, oinv, entry_slot,
+                     t_best, best),
+     ...);
+}
+
+template <typename R, int MAXD, bool FLAT = false, class SIG = NoSig>
 __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 4, "world-space mode is an f32-kernel mode");
     const ConstPrimWorld<float> wp = (ConstPrimWorld<float>)sc.wprims;
@@ -804,6 +826,13 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
         }
     }
     uint32_t k = 0;
+    if constexpr (SIG::n > 0) {  // a scene-specialised kernel (jit.hip): runs known at compile time
+        sig_runs<FLAT>(SIG{}, wp, k, ray, dox, doy, doz, inv, oinv, entry_slot, t_best, best);
+        hm.t = t_best;
+        hm.prim = (uint32_t)best;
+        hm.depth = 0;
+        return best >= 0;
+    }
     for (uint32_t r = 0; r < sc.n_wruns; ++r) {
         const uint32_t run = runs[r];
         const uint32_t kind = run & WRUN_KIND_MASK, count = run >> WRUN_KIND_BITS;
@@ -1470,10 +1499,10 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     return xcands_finish(c, sc, wray, hm);
 }
 
-template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       int32_t* stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0) {
-    if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT>(sc, wray, hm);
+    if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
         if constexpr (PF) {  // plane-only scenes (KF_PLANES)
@@ -1784,7 +1813,7 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // variants that need it: it would raise the register budget of every other scene),
 // KF_FLAT = world-list scene without spheres whose materials all have solid colours
 // (no f64 sphere test, uv mapping or texture lookup compiled in: the Cornell box).
-constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8;
+// (KF_* values: render_params.hpp)
 // KF_PLANES (f64 / ChaCha8 only): the scene has no spheres.  The f64 kernel is register-bound;
 // plane-only scenes run best at 4 waves per SIMD (C5 245 ms, C4 33 ms; 3 waves: 267, 35.5),
 // sphere scenes (f64 quadratic, uv, textures) at 3 (C3 earth 4.85 ms against 5.98 at 4).
@@ -1846,7 +1875,7 @@ struct MatV {
     V<R> color;
 };
 
-template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0>
+template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0, class SIG = NoSig>
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>(KFLAGS)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     constexpr bool PROF = (KFLAGS & KF_PROF) != 0;
@@ -2299,8 +2328,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
                 // world list: the global tables through the scalar cache; records read LDS
                 if (traced)
-                    hit = trace<R, MAXD, EXACT, FLAT>(MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0,
-                                                      p.exact_wbvh != 0);
+                    hit = trace<R, MAXD, EXACT, FLAT, false, SIG>(MAXD == 0 ? gsc : sc, ray, hm, stack,
+                                                                   p.exact_all != 0, p.exact_wbvh != 0);
             }
             const unsigned long long t1 = stamp();
             Rec<R> h;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "device_scene.hpp"
 #include "render_params.hpp"
@@ -22,6 +23,21 @@ void launch_exact(const RenderParams& p, const DSceneView<double>& v, uint32_t r
                   bool planes, hipStream_t stream);
 void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng, int maxd, bool perlin, bool flat,
                  hipStream_t stream);
+// Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
+constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
+
+// Scene-specialised f32 / Philox world-list kernel (jit.hip) for the scene's run words
+// (FlatScene::wruns, at most JIT_MAX_RUNS): a module function, or nullptr when unavailable
+// (NRT_JIT=0, no hiprtc, a compile error); launch_fast_jit enqueues it like launch_fast.
+constexpr size_t JIT_MAX_RUNS = 8;
+struct JitStats {
+    uint64_t compiled = 0;  // kernels built by hiprtc in this process
+    uint64_t launches = 0;  // renders that used one
+};
+void* jit_world_list_kernel(const std::vector<uint32_t>& runs, int kflags, bool lds_scene, int device);
+JitStats jit_stats();
+void launch_fast_jit(const RenderParams& p, const DSceneView<float>& v, void* fn, uint32_t lds_fixed,
+                     hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
                       unsigned long long* d_out);
 

@@ -5,11 +5,10 @@
 #include <stdexcept>
 
 #include "kernel.hpp"
+#include "launch.hpp"
 
 namespace nrt {
 
-// Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
-constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 
 // Blocks the device keeps resident for one kernel variant.
 template <typename K>
@@ -28,8 +27,38 @@ static uint64_t resident_blocks(K kernel, uint32_t lds_bytes) {
 // smallest power of two with >= 1024 samples per group (a group must outlast the
 // longest path in flight for the ring of two to keep lanes busy; small groups keep
 // a wave's rays on few pixels), halved while the launch has fewer than two groups
-// per resident wave (or fewer than 16 while groups keep > 512 samples).  ChaCha8:
-// one lane per pixel.
+// per resident wave (or fewer than 16 while groups keep > 512 samples).
+// `resident(lds)` = blocks the device keeps resident with `lds` bytes of dynamic LDS,
+// `launch(blocks, lds, params)` enqueues the kernel (a static instantiation or a
+// scene-specialised module function, jit.hip).
+template <int MAXD, class Resident, class Launch>
+static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&& resident, Launch&& launch) {
+    const uint32_t npix = p0.pixel_end - p0.pixel_begin;
+    RenderParams p = p0;
+    auto ring_bytes = [](uint32_t wp) { return dev::philox_pool_bytes<MAXD>(wp); };
+    uint32_t wp = p.wave_pixels;
+    if (!wp) {
+        wp = 1;
+        while (wp < 64 && (uint64_t)wp * p.spp < 1024) wp <<= 1;
+        const uint64_t w0 = resident(lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
+        // halve while the launch has fewer than two groups per resident wave, or
+        // (down to 512 samples per group) fewer than 16: the last groups to finish
+        // set the tail, which matters for the short launches of a row shard
+        // (C5 at N = 8: 4.6 -> 9.1 groups per wave, -5 % kernel time)
+        auto groups = [&](uint32_t w) { return (uint64_t)(npix + w - 1) / w; };
+        while (wp > 1 && (groups(wp) < 2 * w0 || ((uint64_t)wp * p.spp > 512 && groups(wp) < 16 * w0))) wp >>= 1;
+    }
+    const uint64_t waves_res = resident(lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
+    p.wave_pixels = wp;
+    p.wave_pixels_log2 = 0;
+    while ((1u << p.wave_pixels_log2) < wp) ++p.wave_pixels_log2;
+    p.groups = (npix + wp - 1) / wp;
+    const uint64_t need = ((uint64_t)p.groups + dev::BLOCK / 64 - 1) / (dev::BLOCK / 64);
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min(waves_res / (dev::BLOCK / 64), need));
+    launch(blocks, lds_fixed + ring_bytes(wp), p);
+}
+
+// ChaCha8: one lane per pixel.
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS>
 static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint32_t lds_fixed, hipStream_t stream) {
     auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, KFLAGS>;
@@ -37,28 +66,11 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
     if constexpr (G::exact_stream) {
         hipLaunchKernelGGL(kernel, dim3((npix + dev::BLOCK - 1) / dev::BLOCK), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
     } else {
-        RenderParams p = p0;
-        auto ring_bytes = [](uint32_t wp) { return dev::philox_pool_bytes<MAXD>(wp); };
-        uint32_t wp = p.wave_pixels;
-        if (!wp) {
-            wp = 1;
-            while (wp < 64 && (uint64_t)wp * p.spp < 1024) wp <<= 1;
-            const uint64_t w0 = resident_blocks(kernel, lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
-            // halve while the launch has fewer than two groups per resident wave, or
-            // (down to 512 samples per group) fewer than 16: the last groups to finish
-            // set the tail, which matters for the short launches of a row shard
-            // (C5 at N = 8: 4.6 -> 9.1 groups per wave, -5 % kernel time)
-            auto groups = [&](uint32_t w) { return (uint64_t)(npix + w - 1) / w; };
-            while (wp > 1 && (groups(wp) < 2 * w0 || ((uint64_t)wp * p.spp > 512 && groups(wp) < 16 * w0))) wp >>= 1;
-        }
-        const uint64_t waves_res = resident_blocks(kernel, lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
-        p.wave_pixels = wp;
-        p.wave_pixels_log2 = 0;
-        while ((1u << p.wave_pixels_log2) < wp) ++p.wave_pixels_log2;
-        p.groups = (npix + wp - 1) / wp;
-        const uint64_t need = ((uint64_t)p.groups + dev::BLOCK / 64 - 1) / (dev::BLOCK / 64);
-        const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min(waves_res / (dev::BLOCK / 64), need));
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(dev::BLOCK), lds_fixed + ring_bytes(wp), stream, p, v);
+        philox_launch<MAXD>(
+            p0, lds_fixed, [&](uint32_t lds) { return resident_blocks(kernel, lds); },
+            [&](uint32_t blocks, uint32_t lds, const RenderParams& p) {
+                hipLaunchKernelGGL(kernel, dim3(blocks), dim3(dev::BLOCK), lds, stream, p, v);
+            });
     }
 }
 

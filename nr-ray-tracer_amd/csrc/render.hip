@@ -54,6 +54,7 @@ struct DeviceScene {
     bool flat = false;      // world list without spheres, solid colours only (KF_FLAT variants)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
+    std::vector<uint32_t> wruns;  // the world list's run words (scene-specialised kernel, jit.hip)
     // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS sets of
     // QUEUE_HEADS per-XCD heads and zeroes it on its own stream (up to QUEUE_SLOTS
     // launches may be in flight at once).
@@ -115,7 +116,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
         auto* mfast = (DMatFast*)track(upload(fs.mats_fast, "mats_fast"), fs.mats_fast.size() * sizeof(DMatFast));
         auto* wpr = (DPrimWorld<float>*)track(upload(f32.wprims, "wprims"), f32.wprims.size() * sizeof(DPrimWorld<float>));
-        auto* wrn = (uint32_t*)track(upload(fs.wruns, "wruns"), fs.wruns.size() * sizeof(uint32_t));
+        std::vector<uint32_t> wruns_padded = fs.wruns;  // whole 16-B groups (run words read 4 at a time)
+        wruns_padded.resize((fs.wruns.size() + 3) & ~size_t(3), 0u);
+        auto* wrn = (uint32_t*)track(upload(wruns_padded, "wruns"), wruns_padded.size() * sizeof(uint32_t));
         auto* wbn = (DBvhNode*)track(upload(fs.wbvh.nodes, "wbvh"), fs.wbvh.nodes.size() * sizeof(DBvhNode));
         auto* wb4 = (DBvh4Node*)track(upload(fs.wbvh.nodes4, "wbvh4"), fs.wbvh.nodes4.size() * sizeof(DBvh4Node));
         auto* wbp = (DPrimWorld<float>*)track(upload(f32.wbvh_prims, "wbvh_prims"),
@@ -173,6 +176,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         ds->world_ok = fs.world_ok;
         ds->list_ok = fs.list_ok;
         ds->world_units = fs.world_units;
+        ds->wruns = fs.wruns;
     } catch (...) {
         gpu_free_scene(ds);
         throw;
@@ -244,9 +248,20 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         } else {
             v.n_wprims = 0;
         }
-        launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
+        void* jit = nullptr;  // the world list's scene-specialised kernel (jit.hip)
+        const uint32_t scene_lds = lds_scene_bytes(v);
+        if (maxd == MODE_WORLD_LIST && rng == RNG_PHILOX && !ds->perlin && !q.counters)
+            jit = jit_world_list_kernel(ds->wruns, ds->flat ? dev::KF_FLAT : 0, scene_lds <= LDS_SCENE_LIMIT,
+                                        ds->device);
+        if (jit) launch_fast_jit(q, v, jit, scene_lds <= LDS_SCENE_LIMIT ? scene_lds : 0u, stream);
+        else launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
     }
     check(hipGetLastError(), "render kernel launch");
+}
+
+JitCounts gpu_jit_counts() {
+    const JitStats s = jit_stats();
+    return JitCounts{s.compiled, s.launches};
 }
 
 void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out) {

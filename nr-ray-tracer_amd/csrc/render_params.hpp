@@ -1,7 +1,9 @@
 // Launch parameters of the path-tracing megakernel (host <-> device POD).
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <cstdint>
+#endif
 
 namespace nrt {
 
@@ -14,6 +16,13 @@ enum : uint32_t { RNG_CHACHA8 = 0, RNG_PHILOX = 1, RNG_PHILOX2_BLOCK = 2 /* nrt_
 // spp <= 2^24 and steps 0..255 (camera 0, scatters 1..max_bounces, defocus 255).
 constexpr uint32_t PHILOX2_STEPS = 256, PHILOX2_MAX_SPP = 1u << 24;
 constexpr uint32_t PHILOX2_MAX_BOUNCES = PHILOX2_STEPS - 2u;
+
+namespace dev {
+// Kernel variant flags (render_kernel's KFLAGS): KF_PROF = phase-profile stamps (diagnostics),
+// KF_PERLIN = the scene has Noise / Marble textures, KF_FLAT = world-mode scene without spheres
+// whose materials all have solid colours, KF_PLANES = f64 kernel, no spheres (kernel.hpp).
+constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8;
+}  // namespace dev
 
 struct RenderParams {
     // Camera after CameraBuilder::build (camera.rs:205-227), always f64 on the host.

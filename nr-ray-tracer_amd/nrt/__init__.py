@@ -80,6 +80,7 @@ _D3 = C.POINTER(C.c_double)
 SIGNATURES = {
     "nrt_abi_version": (C.c_int, []),
     "nrt_build_id": (C.c_char_p, []),
+    "nrt_jit_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
     "nrt_last_error": (C.c_char_p, []),
     "nrt_device_count": (C.c_int, []),
     "nrt_camera_builder_default": (None, [C.POINTER(_CameraBuilder)]),
@@ -177,6 +178,13 @@ def device_count() -> int:
 def build_id() -> str:
     """sha256 prefix of the sources the loaded libnrt.so was built from (nrt_build_id)."""
     return lib().nrt_build_id().decode()
+
+
+def jit_stats() -> dict:
+    """Scene-specialised world-list kernels (nrt_jit_stats): built in this process, renders using one."""
+    out = (C.c_uint64 * 2)()
+    _check(lib().nrt_jit_stats(out))
+    return {"compiled": int(out[0]), "launches": int(out[1])}
 
 
 def source_hash(pkg_dir: Optional[str] = None) -> str:

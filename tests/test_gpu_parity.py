@@ -86,6 +86,30 @@ def test_philox2x32_render_blocks(pixel0, sample):
             assert int(got[lane, step]) == lo | (hi << 32), (lane, step)
 
 
+@pytest.mark.parametrize("scene", ["scenes/cornell-box-scene.json", "scenes/cube-scene.json", "scenes/quads.toml"])
+def test_scene_specialised_kernel_matches_generic(monkeypatch, scene):
+    """The hiprtc-built world-list kernel (jit.hip: the scene's runs as template arguments) is
+    the generic kernel's code with the run loop unrolled: same Philox draws, same exact pixel
+    sums.  Both contract a*b+c into FMAs where the backend sees fit (-ffp-contract=fast), and
+    the unrolled code fuses a few operations differently, so a path can part at the ulp level:
+    on the full C5 frame 3 of 1,048,576 pixels differ (scripts/jit_compare.py; with
+    -ffp-contract=on the frames are identical and the kernel 3 % slower).  At this size the
+    frames agree bit for bit."""
+    s = load(scene, 40, 30, 64)
+    if s.stats()["world_prims"] == 0 or not s.stats()["world_list_ok"]:
+        pytest.skip("scene does not run the world list")
+    monkeypatch.setenv("NRT_JIT", "0")
+    before = nrt.jit_stats()
+    generic = s.render(precision="f32", rng="philox", trace="world-list")
+    assert nrt.jit_stats()["launches"] == before["launches"]
+    monkeypatch.setenv("NRT_JIT", "1")
+    jit = s.render(precision="f32", rng="philox", trace="world-list")
+    assert nrt.jit_stats()["launches"] == before["launches"] + 1, "scene-specialised kernel not used"
+    assert np.isfinite(jit).all() and jit.max() > 0
+    same = np.mean(jit.view(np.uint32) == generic.view(np.uint32))
+    assert same == 1.0, f"{same:.4f} of the values identical"
+
+
 def test_f32_philox_counter_limits():
     # the Philox2x32 counter holds the sample in 24 bits and the path step in 8 (nrt.h)
     with pytest.raises(nrt.NrtError):
