@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gputest_full.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/gputest_full.log; [ $rc = 0 ] || exit 1
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/r02_bench_default.json 2> gpurun_out/r02_bench_default.err || { tail -5 gpurun_out/r02_bench_default.err; exit 1; }
+cat gpurun_out/r02_bench_default.json | cut -c1-400
+bash scripts/configs_bench.sh r02cfg
