@@ -791,10 +791,22 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
 // unit's test and scalar loads known at compile time.  NoSig: the generic loop over sc.wruns.
 struct NoSig {
     static constexpr uint32_t n = 0;
+    static constexpr int bvh = 0;  // world-BVH width known at compile time (BvhSig), 0: read sc.wbvh4
+    static constexpr bool tie = false;
 };
 template <uint32_t... RUNS>
 struct WorldSig {
     static constexpr uint32_t n = sizeof...(RUNS);
+    static constexpr int bvh = 0;
+    static constexpr bool tie = false;
+};
+// World-BVH mode (jit.hip): the tree's width (2 or 4) and whether it holds coplanar-tie
+// keys (WFLAG_COPLANAR) as constants, so one traversal variant is compiled instead of four.
+template <int WIDTH, bool TIE>
+struct BvhSig {
+    static constexpr uint32_t n = 0;
+    static constexpr int bvh = WIDTH;
+    static constexpr bool tie = TIE;
 };
 template <bool FLAT, uint32_t... RUNS>
 __device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float> wp, uint32_t& k, const Ray<float>& ray,
@@ -1139,9 +1151,14 @@ template <typename R>
 __device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
     return sc.wbvh4 ? sc.wbvh4_root : sc.wbvh_root;
 }
-template <typename R, bool FLAT = false>
+template <typename R, bool FLAT = false, class SIG = NoSig>
 __device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack,
                                           unsigned long long* pc = nullptr) {
+    if constexpr (SIG::bvh != 0) {  // a scene-specialised kernel (jit.hip)
+        if constexpr (FLAT && NRT_WBVH_IFIF) wbvh_trip_impl<R, SIG::bvh == 4, FLAT, SIG::tie>(ts, sc, ray, stack, pc);
+        else wbvh_round_impl<R, SIG::bvh == 4, FLAT>(ts, sc, ray, stack, pc);
+        return;
+    }
     if constexpr (FLAT && NRT_WBVH_IFIF) {
         if (sc.wbvh4) wbvh_trip<R, true, FLAT>(ts, sc, ray, stack, pc);
         else wbvh_trip<R, false, FLAT>(ts, sc, ray, stack, pc);
@@ -2312,7 +2329,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = alive && ts.busy();
                     if (__ballot(going) == 0ull) break;
                     if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
+                    if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
                 }
                 sh = alive && !ts.busy();
                 if constexpr (PROF) {

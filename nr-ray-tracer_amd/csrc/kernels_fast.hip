@@ -21,27 +21,29 @@ void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng
     else launch_fast_rng<dev::Philox>(p, v, maxd, perlin, flat, stream);
 }
 
-void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* fnp, uint32_t lds_fixed,
+void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* fnp, uint32_t lds_fixed, int maxd,
                      hipStream_t stream) {
     const hipFunction_t fn = (hipFunction_t)fnp;
-    philox_launch<MODE_WORLD_LIST>(
-        p0, lds_fixed,
-        [&](uint32_t lds) {
-            int per_cu = 0, dev_id = 0, cus = 0;
-            if (hipGetDevice(&dev_id) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
-                hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, dev::BLOCK, lds) != hipSuccess ||
-                per_cu <= 0 || cus <= 0)
-                throw std::runtime_error("occupancy query failed for the scene-specialised kernel");
-            return (uint64_t)per_cu * (uint64_t)cus;
-        },
-        [&](uint32_t blocks, uint32_t lds, const RenderParams& p) {
-            RenderParams pp = p;
-            DSceneView<float> vv = v;
-            void* args[] = {&pp, &vv};
-            if (hipModuleLaunchKernel(fn, blocks, 1, 1, dev::BLOCK, 1, 1, lds, stream, args, nullptr) != hipSuccess)
-                throw std::runtime_error("HIP error in hipModuleLaunchKernel (scene-specialised kernel)");
-        });
+    auto resident = [&](uint32_t lds) {
+        int per_cu = 0, dev_id = 0, cus = 0;
+        if (hipGetDevice(&dev_id) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
+            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, dev::BLOCK, lds) != hipSuccess ||
+            per_cu <= 0 || cus <= 0)
+            throw std::runtime_error("occupancy query failed for the scene-specialised kernel");
+        return (uint64_t)per_cu * (uint64_t)cus;
+    };
+    auto launch = [&](uint32_t blocks, uint32_t lds, const RenderParams& p) {
+        RenderParams pp = p;
+        DSceneView<float> vv = v;
+        void* args[] = {&pp, &vv};
+        if (hipModuleLaunchKernel(fn, blocks, 1, 1, dev::BLOCK, 1, 1, lds, stream, args, nullptr) != hipSuccess)
+            throw std::runtime_error("HIP error in hipModuleLaunchKernel (scene-specialised kernel)");
+    };
+    if (maxd == MODE_WORLD_BVH)  // below the staged scene: the traversal stack (launch_one's ring)
+        philox_launch<MODE_WORLD_BVH>(p0, lds_fixed + (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t),
+                                      resident, launch);
+    else philox_launch<MODE_WORLD_LIST>(p0, lds_fixed, resident, launch);
 }
 
 }  // namespace nrt

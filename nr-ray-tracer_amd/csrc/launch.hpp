@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "device_scene.hpp"
@@ -26,17 +27,18 @@ void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng
 // Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
 constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 
-// Scene-specialised f32 / Philox world-list kernel (jit.hip) for the scene's run words
-// (FlatScene::wruns, at most JIT_MAX_RUNS): a module function, or nullptr when unavailable
-// (NRT_JIT=0, no hiprtc, a compile error); launch_fast_jit enqueues it like launch_fast.
-constexpr size_t JIT_MAX_RUNS = 8;
+// Scene-specialised f32 / Philox kernels (jit.hip): render_kernel<targs> built with hiprtc, a
+// module function, or nullptr when unavailable (NRT_JIT=0, no hiprtc, a compile error);
+// launch_fast_jit enqueues it like launch_fast (maxd: MODE_WORLD_LIST or MODE_WORLD_BVH;
+// lds_fixed = the staged scene's bytes, the BVH stack is added there).
+constexpr size_t JIT_MAX_RUNS = 8;  // world lists with more runs keep the generic loop
 struct JitStats {
     uint64_t compiled = 0;  // kernels built by hiprtc in this process
     uint64_t launches = 0;  // renders that used one
 };
-void* jit_world_list_kernel(const std::vector<uint32_t>& runs, int kflags, bool lds_scene, int device);
+void* jit_render_kernel(const std::string& targs, int device);
 JitStats jit_stats();
-void launch_fast_jit(const RenderParams& p, const DSceneView<float>& v, void* fn, uint32_t lds_fixed,
+void launch_fast_jit(const RenderParams& p, const DSceneView<float>& v, void* fn, uint32_t lds_fixed, int maxd,
                      hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
                       unsigned long long* d_out);

@@ -248,12 +248,28 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         } else {
             v.n_wprims = 0;
         }
-        void* jit = nullptr;  // the world list's scene-specialised kernel (jit.hip)
+        // scene-specialised kernel (jit.hip): the world list's run words, or the world BVH's
+        // width and tie flag, as template arguments; the same LDS layout as launch_one
+        void* jit = nullptr;
         const uint32_t scene_lds = lds_scene_bytes(v);
-        if (maxd == MODE_WORLD_LIST && rng == RNG_PHILOX && !ds->perlin && !q.counters)
-            jit = jit_world_list_kernel(ds->wruns, ds->flat ? dev::KF_FLAT : 0, scene_lds <= LDS_SCENE_LIMIT,
-                                        ds->device);
-        if (jit) launch_fast_jit(q, v, jit, scene_lds <= LDS_SCENE_LIMIT ? scene_lds : 0u, stream);
+        const bool staged = scene_lds <= LDS_SCENE_LIMIT;
+        const uint32_t lds_fixed = staged ? scene_lds : 0u;  // (+ the BVH stack: launch_fast_jit)
+        if ((maxd == MODE_WORLD_LIST || maxd == MODE_WORLD_BVH) && rng == RNG_PHILOX && !ds->perlin && !q.counters) {
+            std::string targs = "float, nrt::dev::Philox, " + std::to_string(maxd) + ", false, " +
+                                (staged ? "true, " : "false, ") + std::to_string(ds->flat ? dev::KF_FLAT : 0) + ", ";
+            if (maxd == MODE_WORLD_LIST) {
+                if (!ds->wruns.empty() && ds->wruns.size() <= JIT_MAX_RUNS) {
+                    targs += "nrt::dev::WorldSig<";
+                    for (size_t i = 0; i < ds->wruns.size(); ++i) targs += (i ? ", " : "") + std::to_string(ds->wruns[i]) + "u";
+                    jit = jit_render_kernel(targs + ">", ds->device);
+                }
+            } else if (ds->flat) {  // (if-if trips: teapot 41.1 -> 40.5 ms; the sphere rounds measured slower)
+                targs += std::string("nrt::dev::BvhSig<") + (v.wbvh4 ? "4, " : "2, ") +
+                         ((v.wflags & WFLAG_COPLANAR) ? "true>" : "false>");
+                jit = jit_render_kernel(targs, ds->device);
+            }
+        }
+        if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, stream);
         else launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
     }
     check(hipGetLastError(), "render kernel launch");
