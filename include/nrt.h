@@ -150,6 +150,9 @@ const char* nrt_build_id(void);
  * f32 / Philox world-list mode; NRT_JIT=0 turns them off): out[0] = kernels built in this
  * process, out[1] = renders that used one.  No reference counterpart. */
 int nrt_jit_stats(uint64_t out[2]);
+/* Tests: compile render_kernel<targs> with hiprtc from the embedded headers, no GPU needed
+ * (nothing is loaded); *code_bytes = the code object's size. */
+int nrt_debug_jit_compile(const char* targs, uint64_t* code_bytes);
 const char* nrt_last_error(void);   /* thread-local; message text mirrors anyhow's */
 int nrt_device_count(void);
 

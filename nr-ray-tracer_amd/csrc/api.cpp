@@ -316,6 +316,16 @@ int nrt_abi_version(void) { return NRT_ABI_VERSION; }
 #endif
 const char* nrt_build_id(void) { return NRT_SRC_HASH; }
 
+int nrt_debug_jit_compile(const char* targs, uint64_t* code_bytes) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!targs || !code_bytes) throw std::invalid_argument("null argument");
+        std::string log;
+        *code_bytes = gpu_jit_compile_only(targs, &log);
+        if (!*code_bytes) throw std::runtime_error("hiprtc: " + log.substr(0, 2000));
+        return NRT_OK;
+    });
+}
+
 int nrt_jit_stats(uint64_t out[2]) {
     return guarded(NRT_E_INVALID, [&]() {
         if (!out) throw std::invalid_argument("null output");

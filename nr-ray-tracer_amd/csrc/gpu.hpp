@@ -3,6 +3,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <string>
 
 #include "render_params.hpp"
 
@@ -26,6 +27,7 @@ struct JitCounts {
     uint64_t compiled, launches;
 };
 JitCounts gpu_jit_counts();  // scene-specialised kernels (jit.hip)
+uint64_t gpu_jit_compile_only(const char* targs, std::string* log);
 void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out);
 
 }  // namespace nrt

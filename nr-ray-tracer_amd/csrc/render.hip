@@ -275,6 +275,8 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     check(hipGetLastError(), "render kernel launch");
 }
 
+uint64_t gpu_jit_compile_only(const char* targs, std::string* log) { return jit_compile_only(targs, log); }
+
 JitCounts gpu_jit_counts() {
     const JitStats s = jit_stats();
     return JitCounts{s.compiled, s.launches};

@@ -81,6 +81,7 @@ SIGNATURES = {
     "nrt_abi_version": (C.c_int, []),
     "nrt_build_id": (C.c_char_p, []),
     "nrt_jit_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
+    "nrt_debug_jit_compile": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     "nrt_last_error": (C.c_char_p, []),
     "nrt_device_count": (C.c_int, []),
     "nrt_camera_builder_default": (None, [C.POINTER(_CameraBuilder)]),
@@ -185,6 +186,13 @@ def jit_stats() -> dict:
     out = (C.c_uint64 * 2)()
     _check(lib().nrt_jit_stats(out))
     return {"compiled": int(out[0]), "launches": int(out[1])}
+
+
+def debug_jit_compile(targs: str) -> int:
+    """hiprtc-compile render_kernel<targs> from the library's embedded headers (no GPU): code bytes."""
+    n = C.c_uint64(0)
+    _check(lib().nrt_debug_jit_compile(targs.encode(), C.byref(n)))
+    return int(n.value)
 
 
 def source_hash(pkg_dir: Optional[str] = None) -> str:

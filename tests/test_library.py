@@ -173,3 +173,17 @@ def test_library_built_from_these_sources():
     """Build provenance: the loaded libnrt.so carries the hash of the sources it was
     compiled from; it must equal the hash of csrc/ + include/nrt.h in this tree."""
     assert nrt.build_id() == nrt.source_hash()
+
+
+@pytest.mark.parametrize("targs", [
+    # Cornell's world list (ABOX x1, QUAD_Y x1, BOXY x2), KF_FLAT, scene staged in LDS
+    "float, nrt::dev::Philox, 0, false, true, 4, nrt::dev::WorldSig<23u, 21u, 40u>",
+    # the teapot's world BVH (4-wide, no coplanar ties), KF_FLAT, unstaged
+    "float, nrt::dev::Philox, -1, false, false, 4, nrt::dev::BvhSig<4, false>",
+])
+def test_scene_specialised_kernel_compiles(targs):
+    """The device headers embedded in libnrt.so still compile under hiprtc (jit.hip), so a GPU
+    run builds the scene-specialised kernels instead of falling back to the generic ones."""
+    assert nrt.debug_jit_compile(targs) > 4096
+    with pytest.raises(nrt.NrtError):
+        nrt.debug_jit_compile("float, nrt::dev::NoSuchRng, 0")
