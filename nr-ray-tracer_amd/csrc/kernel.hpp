@@ -1168,13 +1168,13 @@ __device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc,
     }
 }
 
-template <typename R, int MAXD, bool FLAT = false>
+template <typename R, int MAXD, bool FLAT = false, class SIG = NoSig>
 __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm,
                                                 int32_t* stack) {
     static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), ray);
-    while (ts.busy()) wbvh_step<R, FLAT>(ts, sc, ray, stack);
+    while (ts.busy()) wbvh_step<R, FLAT, SIG>(ts, sc, ray, stack);
     hm.t = ts.t_best;
     hm.prim = (uint32_t)ts.best;
     hm.depth = 0;
@@ -1520,7 +1520,7 @@ template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, 
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       int32_t* stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
-    else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT>(sc, wray, hm, stack);
+    else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8) {
         if constexpr (PF) {  // plane-only scenes (KF_PLANES)
             if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm);
@@ -2150,7 +2150,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
-                    hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0>(
+                    hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0, SIG>(
                         MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf);
                     t2 = stamp();
                 }

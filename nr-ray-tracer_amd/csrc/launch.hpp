@@ -27,10 +27,10 @@ void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng
 // Scenes whose node/prim/xform/material tables fit stay in LDS for the whole launch.
 constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 
-// Scene-specialised f32 / Philox kernels (jit.hip): render_kernel<targs> built with hiprtc, a
-// module function, or nullptr when unavailable (NRT_JIT=0, no hiprtc, a compile error);
-// launch_fast_jit enqueues it like launch_fast (maxd: MODE_WORLD_LIST or MODE_WORLD_BVH;
-// lds_fixed = the staged scene's bytes, the BVH stack is added there).
+// Scene-specialised f32 kernels (jit.hip; Philox or ChaCha8): render_kernel<targs> built with
+// hiprtc, a module function, or nullptr when unavailable (NRT_JIT=0, no hiprtc, a compile
+// error); launch_fast_jit enqueues it like launch_fast (maxd: MODE_WORLD_LIST or MODE_WORLD_BVH;
+// lds_fixed = the staged scene's bytes, the ChaCha8 ring and the BVH stack are added there).
 constexpr size_t JIT_MAX_RUNS = 8;  // world lists with more runs keep the generic loop
 struct JitStats {
     uint64_t compiled = 0;  // kernels built by hiprtc in this process
@@ -40,7 +40,7 @@ void* jit_render_kernel(const std::string& targs, int device);
 JitStats jit_stats();
 uint64_t jit_compile_only(const std::string& targs, std::string* log);  // code bytes, 0 on failure (tests)
 void launch_fast_jit(const RenderParams& p, const DSceneView<float>& v, void* fn, uint32_t lds_fixed, int maxd,
-                     hipStream_t stream);
+                     uint32_t rng, hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
                       unsigned long long* d_out);
 

@@ -254,11 +254,15 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         const uint32_t scene_lds = lds_scene_bytes(v);
         const bool staged = scene_lds <= LDS_SCENE_LIMIT;
         const uint32_t lds_fixed = staged ? scene_lds : 0u;  // (+ the BVH stack: launch_fast_jit)
-        if ((maxd == MODE_WORLD_LIST || maxd == MODE_WORLD_BVH) && rng == RNG_PHILOX && !ds->perlin && !q.counters) {
-            std::string targs = "float, nrt::dev::Philox, " + std::to_string(maxd) + ", false, " +
+        if ((maxd == MODE_WORLD_LIST || maxd == MODE_WORLD_BVH) && (rng == RNG_PHILOX || rng == RNG_CHACHA8) &&
+            !ds->perlin && !q.counters) {
+            std::string targs = std::string("float, nrt::dev::") + (rng == RNG_PHILOX ? "Philox, " : "ChaCha8, ") +
+                                std::to_string(maxd) + ", false, " +
                                 (staged ? "true, " : "false, ") + std::to_string(ds->flat ? dev::KF_FLAT : 0) + ", ";
             if (maxd == MODE_WORLD_LIST) {
-                if (!ds->wruns.empty() && ds->wruns.size() <= JIT_MAX_RUNS) {
+                // ChaCha8 keeps the generic world-list kernel: its specialised build measured
+                // 1.85x slower on C5 (72 -> 133 ms), the Philox one 1.25x faster
+                if (rng == RNG_PHILOX && !ds->wruns.empty() && ds->wruns.size() <= JIT_MAX_RUNS) {
                     targs += "nrt::dev::WorldSig<";
                     for (size_t i = 0; i < ds->wruns.size(); ++i) targs += (i ? ", " : "") + std::to_string(ds->wruns[i]) + "u";
                     jit = jit_render_kernel(targs + ">", ds->device);
@@ -269,7 +273,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
                 jit = jit_render_kernel(targs, ds->device);
             }
         }
-        if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, stream);
+        if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, rng, stream);
         else launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
     }
     check(hipGetLastError(), "render kernel launch");

@@ -90,10 +90,12 @@ def test_philox2x32_render_blocks(pixel0, sample):
                                          ("scenes/cube-scene.json", "world-list"), ("scenes/quads.toml", "world-list"),
                                          ("scenes/utah-teapot-scene.json", "world-bvh"),
                                          ("scenes/spheres.toml", "world-bvh"), ("scenes/cornell-box-scene.json", "world-bvh")])
-def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace):
+@pytest.mark.parametrize("rng", ["philox", "chacha8"])
+def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace, rng):
     """The hiprtc-built kernels (jit.hip: the world list's runs, or the world BVH's width and tie
     flag, as template arguments) are the generic kernel's code with the run loop unrolled or
-    one traversal variant selected: same Philox draws, same exact pixel sums.  Both contract a*b+c into FMAs where the backend sees fit (-ffp-contract=fast), and
+    one traversal variant selected: same Philox draws and exact pixel sums, or the same ChaCha8
+    stream and f64 sum order (one lane per pixel).  Both contract a*b+c into FMAs where the backend sees fit (-ffp-contract=fast), and
     the unrolled code fuses a few operations differently, so a path can part at the ulp level:
     on the full C5 frame 3 of 1,048,576 pixels differ (scripts/jit_compare.py; with
     -ffp-contract=on the frames are identical and the kernel 3 % slower), and the spheres
@@ -104,11 +106,12 @@ def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace):
         pytest.skip("scene does not run this world mode")
     monkeypatch.setenv("NRT_JIT", "0")
     before = nrt.jit_stats()
-    generic = s.render(precision="f32", rng="philox", trace=trace)
+    generic = s.render(precision="f32", rng=rng, trace=trace)
     assert nrt.jit_stats()["launches"] == before["launches"]
     monkeypatch.setenv("NRT_JIT", "1")
-    jit = s.render(precision="f32", rng="philox", trace=trace)
-    if trace == "world-bvh" and scene.endswith("spheres.toml"):  # sphere scenes keep the generic BVH kernel
+    jit = s.render(precision="f32", rng=rng, trace=trace)
+    if (trace == "world-bvh" and scene.endswith("spheres.toml")) or (trace == "world-list" and rng == "chacha8"):
+        # sphere scenes keep the generic BVH kernel, ChaCha8 the generic world-list kernel
         assert nrt.jit_stats()["launches"] == before["launches"]
         np.testing.assert_array_equal(jit, generic)
         return

@@ -180,6 +180,9 @@ def test_library_built_from_these_sources():
     "float, nrt::dev::Philox, 0, false, true, 4, nrt::dev::WorldSig<23u, 21u, 40u>",
     # the teapot's world BVH (4-wide, no coplanar ties), KF_FLAT, unstaged
     "float, nrt::dev::Philox, -1, false, false, 4, nrt::dev::BvhSig<4, false>",
+    # the same two with the reference's ChaCha8 stream (one lane per pixel)
+    "float, nrt::dev::ChaCha8, 0, false, true, 4, nrt::dev::WorldSig<23u, 21u, 40u>",
+    "float, nrt::dev::ChaCha8, -1, false, false, 4, nrt::dev::BvhSig<4, false>",
 ])
 def test_scene_specialised_kernel_compiles(targs):
     """The device headers embedded in libnrt.so still compile under hiprtc (jit.hip), so a GPU
