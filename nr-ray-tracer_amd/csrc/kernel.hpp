@@ -2114,7 +2114,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = active && ts.busy();
                     if (__ballot(going) == 0ull) break;
                     if ((uint32_t)__popcll(__ballot(active && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step<R, FLAT>(ts, gsc, ray, stack);
+                    if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack);
                 }
                 const unsigned long long t1 = stamp();
                 if (active && !ts.busy()) {
