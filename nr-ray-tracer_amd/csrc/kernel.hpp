@@ -793,12 +793,25 @@ struct NoSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = 0;  // world-BVH width known at compile time (BvhSig), 0: read sc.wbvh4
     static constexpr bool tie = false;
+    static constexpr int exact = 0;  // exact kernel: traversal fixed at compile time (ExactSig), 0: runtime
 };
 template <uint32_t... RUNS>
 struct WorldSig {
     static constexpr uint32_t n = sizeof...(RUNS);
     static constexpr int bvh = 0;
     static constexpr bool tie = false;
+    static constexpr int exact = 0;
+};
+// Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
+// the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
+// plane-only scenes, and the unfiltered walk it falls back to).
+enum : int { EXACT_SIG_WORLD_PF = 1 };
+template <int MODE, int WIDTH>
+struct ExactSig {
+    static constexpr uint32_t n = 0;
+    static constexpr int bvh = WIDTH;  // the culling tree's width (2 or 4), 0: sc.wbvh4 at run time
+    static constexpr bool tie = false;
+    static constexpr int exact = MODE;
 };
 // World-BVH mode (jit.hip): the tree's width (2 or 4) and whether it holds coplanar-tie
 // keys (WFLAG_COPLANAR) as constants, so one traversal variant is compiled instead of four.
@@ -807,6 +820,7 @@ struct BvhSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = WIDTH;
     static constexpr bool tie = TIE;
+    static constexpr int exact = 0;
 };
 template <bool FLAT, uint32_t... RUNS>
 __device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float> wp, uint32_t& k, const Ray<float>& ray,
@@ -1303,7 +1317,7 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 // outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
 // inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
 // private array (PrivStack; the LDS holds the ChaCha8 ring and the staged scene).
-template <typename R, int MAXD>
+template <typename R, int MAXD, int W = 0>  // W: tree width fixed at compile time (ExactSig), 0: sc.wbvh4
 __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
@@ -1318,7 +1332,7 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
     Ray<R> oray = wray;
     while (true) {
         while (ts.node >= 0) {
-            if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
+            if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
             else wbvh2_visit<R>(ts, sc, stk);
         }
         if (ts.node == WBVH_DONE) break;
@@ -1488,7 +1502,7 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
 }
 
 // The prefilter over the world-BVH walk (RenderParams::exact_pf).
-template <typename R, int MAXD>
+template <typename R, int MAXD, int W = 0>
 __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
@@ -1502,7 +1516,7 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
         PrivStack stk;
         while (true) {
             while (ts.node >= 0) {
-                if (sc.wbvh4) wbvh4_visit<R>(ts, sc, stk);
+                if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
                 else wbvh2_visit<R>(ts, sc, stk);
             }
             if (ts.node == WBVH_DONE) break;
@@ -1512,7 +1526,7 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
             ts.node = wbvh_pop(ts, stk);
         }
     }
-    if (c.over) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+    if (c.over) return trace_exact_wbvh<R, MAXD, W>(sc, wray, hm);
     return xcands_finish(c, sc, wray, hm);
 }
 
@@ -1521,7 +1535,10 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
                                       int32_t* stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
-    else if constexpr (EXACT && sizeof(R) == 8) {
+    else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
+        static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
+        return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);
+    } else if constexpr (EXACT && sizeof(R) == 8) {
         if constexpr (PF) {  // plane-only scenes (KF_PLANES)
             if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm);
         }
