@@ -206,10 +206,25 @@ def main():
                     help="f32 kernel traversal (nrt_trace): auto = world-space list for small flattenable scenes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = host-side gather, "
+                         "ranks may share a GPU (rehearses the N > 1 step on a one-GPU box)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
+                         "prints one JSON line, no GPU is touched")
     ap.add_argument("--kernel-only", action="store_true",
                     help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
                          "sampled over a render dispatch see the render kernel alone")
     args = ap.parse_args()
+    if args.cpu_only:
+        cpu = cpu_baseline(args)
+        print(json.dumps({"metric": "Msamples/sec (CPU baseline, oracle)", "value": cpu["value"], "unit": "Msamples/s",
+                          "higher_is_better": True, "config": {"workload": f"{os.path.basename(args.scene)} "
+                                                               f"{args.width}x{args.height} spp={args.spp}",
+                                                               "scene": args.scene, "width": args.width,
+                                                               "height": args.height, "spp": args.spp},
+                          "cpu_baseline": cpu}), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -221,10 +236,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world == 1:
         raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {ndev} GPU(s) visible (nccl needs one GPU per rank)")
+    local = local % ndev  # gloo: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     old = os.getcwd()
     os.chdir(os.path.join(ROOT, "tests", "golden"))  # scene files use CWD-relative paths
@@ -274,7 +296,7 @@ def main():
             fr = frames[slot] if lead else None
             if lead and copied[slot] is not None:
                 stream.wait_event(copied[slot])  # frame buffer `slot` was copied out two frames ago
-            shard.gather_frame(buf, H, dist, rank, world, out=fr)
+            shard.gather_frame(buf, H, dist, rank, world, out=fr, host=args.backend == "gloo")
         if lead and not args.kernel_only:
             ready = torch.cuda.Event()
             ready.record(stream)
@@ -292,6 +314,7 @@ def main():
     for k in range(args.warmup):
         step(k, False)
     torch.cuda.synchronize()
+    jit_before = nrt.jit_stats()  # the first render of the scene in a world mode built its kernel (warm-up)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -303,11 +326,18 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in kev) / max(len(kev), 1)
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
+    jit_after = nrt.jit_stats()
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
+    kernel_variant = "scene-specialised (hiprtc)" if jit_after["launches"] - jit_before["launches"] >= args.steps \
+        else "generic"
+    if jit_after["failed"]:
+        kernel_variant = "generic (scene-specialised build FAILED)"
+        print(f"bench.py: WARNING: {jit_after['failed']} scene-specialised kernel build(s) failed; the generic "
+              f"kernel was timed", file=sys.stderr, flush=True)
     if lead:
         last = host[(args.warmup + args.steps - 1) % 2].numpy()
         frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
@@ -360,11 +390,17 @@ def main():
             "work": work_block(wc, value, args.precision),
             "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
                            "frame_wall": round(elapsed / args.steps * 1e3, 3)},
-            "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4)},
+            # the reference times scene.render (render.rs:57-62): a one-shot render of a scene would also pay
+            # the scene-specialised kernel's compile, done here in the warm-up and reported on its own
+            "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4),
+                          "jit_compile": jit_after["compile_s"]},
             "frame_sha256": frame_sha,
             "build_id": nrt.build_id(),  # sha256 prefix of the sources libnrt.so was built from
-            # scene-specialised world-list kernels (jit.hip): built with hiprtc in this process, renders using one
-            "jit": nrt.jit_stats(),
+            # scene-specialised kernels (jit.hip): built with hiprtc in this process, renders using one; the
+            # timed frames ran on one only if every timed launch counted (a failed build falls back to the
+            # generic kernel, which is slower: then the line says so)
+            "jit": dict(jit_after, timed_launches=jit_after["launches"] - jit_before["launches"]),
+            "kernel_variant": kernel_variant,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)

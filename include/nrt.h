@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 3
+#define NRT_ABI_VERSION 4
 
 enum {
     NRT_OK = 0,
@@ -146,10 +146,13 @@ int nrt_abi_version(void);
 /* sha256 prefix of the library's sources it was built from (build provenance; no reference
  * counterpart) */
 const char* nrt_build_id(void);
-/* Scene-specialised world-list kernels (built with hiprtc when a scene is first rendered in
- * f32 / Philox world-list mode; NRT_JIT=0 turns them off): out[0] = kernels built in this
- * process, out[1] = renders that used one.  No reference counterpart. */
-int nrt_jit_stats(uint64_t out[2]);
+/* Scene-specialised kernels (built with hiprtc, loaded lazily, when a scene is first rendered
+ * in an f32 world mode; NRT_JIT=0 turns them off).  The first such render of a scene in a
+ * process pays the compile (~1 s) inside the render call.  out[0] = kernels built in this
+ * process, out[1] = renders that used one, out[2] = builds that failed (the generic kernel
+ * rendered instead: slower, and its f32 frames may differ in the last bits), out[3] = compile
+ * wall time in ns; the first min(n, 4) are written.  No reference counterpart. */
+int nrt_jit_stats(uint64_t* out, size_t n);
 /* Tests: compile render_kernel<targs> with hiprtc from the embedded headers, no GPU needed
  * (nothing is loaded); *code_bytes = the code object's size. */
 int nrt_debug_jit_compile(const char* targs, uint64_t* code_bytes);
@@ -182,6 +185,10 @@ int32_t nrt_material_metal(nrt_builder* b, double fuzz, int32_t texture);       
 int32_t nrt_material_dielectric(nrt_builder* b, double refraction_index);               /* Dielectric::new */
 int32_t nrt_material_diffuse_light(nrt_builder* b, double intensity, int32_t texture);  /* DiffuseLightBuilder */
 int32_t nrt_object_sphere(nrt_builder* b, const double center[3], double radius, int32_t material); /* SphereBuilder */
+/* SphereBuilder::with_speed (lib/objects/sphere.rs:45-50): centre(time) = center + time * speed for the
+ * ray's time in [0, 1) (sphere.rs:110-111, camera.rs:264); the box spans both end positions (sphere.rs:72-84) */
+int32_t nrt_object_sphere_moving(nrt_builder* b, const double center[3], const double speed[3], double radius,
+                                 int32_t material);
 int32_t nrt_object_quad(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material);
 int32_t nrt_object_triangle(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material);
 int32_t nrt_object_bvh(nrt_builder* b, const int32_t* objects, size_t count);          /* BVH::from */

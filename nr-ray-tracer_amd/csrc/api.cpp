@@ -326,12 +326,12 @@ int nrt_debug_jit_compile(const char* targs, uint64_t* code_bytes) {
     });
 }
 
-int nrt_jit_stats(uint64_t out[2]) {
+int nrt_jit_stats(uint64_t* out, size_t n) {
     return guarded(NRT_E_INVALID, [&]() {
-        if (!out) throw std::invalid_argument("null output");
+        if (!out && n) throw std::invalid_argument("null output");
         const JitCounts c = gpu_jit_counts();
-        out[0] = c.compiled;
-        out[1] = c.launches;
+        const uint64_t v[4] = {c.compiled, c.launches, c.failed, c.compile_ns};
+        for (size_t k = 0; k < n && k < 4; ++k) out[k] = v[k];
         return NRT_OK;
     });
 }
@@ -445,6 +445,11 @@ int32_t nrt_material_diffuse_light(nrt_builder* b, double intensity, int32_t tex
 }
 int32_t nrt_object_sphere(nrt_builder* b, const double center[3], double radius, int32_t material) {
     NRT_BUILD(return add_obj(b, make_sphere(v3of(center), radius, mat_at(b, material)));)
+}
+int32_t nrt_object_sphere_moving(nrt_builder* b, const double center[3], const double speed[3], double radius,
+                                 int32_t material) {
+    NRT_BUILD(if (!speed) throw std::invalid_argument("null speed"); const V3 sp = v3of(speed);
+              return add_obj(b, make_sphere(v3of(center), radius, mat_at(b, material), &sp));)
 }
 int32_t nrt_object_quad(nrt_builder* b, const double p[3], const double u[3], const double v[3], int32_t material) {
     NRT_BUILD(return add_obj(b, make_plane(Object::Quad, v3of(p), v3of(u), v3of(v), mat_at(b, material)));)

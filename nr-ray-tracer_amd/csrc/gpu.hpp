@@ -24,7 +24,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
 int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace);
 // First `count` draws of `lanes` consecutive streams starting at stream0 (tests).
 struct JitCounts {
-    uint64_t compiled, launches;
+    uint64_t compiled, launches, failed, compile_ns;
 };
 JitCounts gpu_jit_counts();  // scene-specialised kernels (jit.hip)
 uint64_t gpu_jit_compile_only(const char* targs, std::string* log);

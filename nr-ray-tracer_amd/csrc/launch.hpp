@@ -33,8 +33,10 @@ constexpr uint32_t LDS_SCENE_LIMIT = 64 * 1024;
 // lds_fixed = the staged scene's bytes, the ChaCha8 ring and the BVH stack are added there).
 constexpr size_t JIT_MAX_RUNS = 8;  // world lists with more runs keep the generic loop
 struct JitStats {
-    uint64_t compiled = 0;  // kernels built by hiprtc in this process
-    uint64_t launches = 0;  // renders that used one
+    uint64_t compiled = 0;    // kernels built by hiprtc in this process
+    uint64_t launches = 0;    // renders that used one
+    uint64_t failed = 0;      // builds that failed (the generic kernel ran instead)
+    uint64_t compile_ns = 0;  // wall time spent in hiprtc + module load
 };
 void* jit_render_kernel(const std::string& targs, int device);
 JitStats jit_stats();

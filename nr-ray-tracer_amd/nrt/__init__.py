@@ -80,7 +80,7 @@ _D3 = C.POINTER(C.c_double)
 SIGNATURES = {
     "nrt_abi_version": (C.c_int, []),
     "nrt_build_id": (C.c_char_p, []),
-    "nrt_jit_stats": (C.c_int, [C.POINTER(C.c_uint64)]),
+    "nrt_jit_stats": (C.c_int, [C.POINTER(C.c_uint64), C.c_size_t]),
     "nrt_debug_jit_compile": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     "nrt_last_error": (C.c_char_p, []),
     "nrt_device_count": (C.c_int, []),
@@ -101,6 +101,7 @@ SIGNATURES = {
     "nrt_material_dielectric": (C.c_int32, [C.c_void_p, C.c_double]),
     "nrt_material_diffuse_light": (C.c_int32, [C.c_void_p, C.c_double, C.c_int32]),
     "nrt_object_sphere": (C.c_int32, [C.c_void_p, _D3, C.c_double, C.c_int32]),
+    "nrt_object_sphere_moving": (C.c_int32, [C.c_void_p, _D3, _D3, C.c_double, C.c_int32]),
     "nrt_object_quad": (C.c_int32, [C.c_void_p, _D3, _D3, _D3, C.c_int32]),
     "nrt_object_triangle": (C.c_int32, [C.c_void_p, _D3, _D3, _D3, C.c_int32]),
     "nrt_object_bvh": (C.c_int32, [C.c_void_p, C.POINTER(C.c_int32), C.c_size_t]),
@@ -182,10 +183,12 @@ def build_id() -> str:
 
 
 def jit_stats() -> dict:
-    """Scene-specialised world-list kernels (nrt_jit_stats): built in this process, renders using one."""
-    out = (C.c_uint64 * 2)()
-    _check(lib().nrt_jit_stats(out))
-    return {"compiled": int(out[0]), "launches": int(out[1])}
+    """Scene-specialised kernels (nrt_jit_stats): built in this process, renders using one, builds that
+    failed (the generic kernel rendered instead), seconds spent compiling."""
+    out = (C.c_uint64 * 4)()
+    _check(lib().nrt_jit_stats(out, 4))
+    return {"compiled": int(out[0]), "launches": int(out[1]), "failed": int(out[2]),
+            "compile_s": round(int(out[3]) * 1e-9, 4)}
 
 
 def debug_jit_compile(targs: str) -> int:
@@ -475,7 +478,10 @@ class Builder:
     def diffuse_light(self, intensity: float, tex: int) -> int:
         return _handle(lib().nrt_material_diffuse_light(self._b, intensity, tex))
 
-    def sphere(self, center, radius: float, mat: int) -> int:
+    def sphere(self, center, radius: float, mat: int, speed=None) -> int:
+        """SphereBuilder; `speed` = SphereBuilder::with_speed (sphere.rs:45-50): a moving sphere."""
+        if speed is not None:
+            return _handle(lib().nrt_object_sphere_moving(self._b, _d3(center), _d3(speed), radius, mat))
         return _handle(lib().nrt_object_sphere(self._b, _d3(center), radius, mat))
 
     def quad(self, p, u, v, mat: int) -> int:

@@ -31,13 +31,22 @@ def assemble(gathered: List["torch.Tensor"], height: int) -> "torch.Tensor":
 _staging = {}
 
 
-def gather_frame(buf: "torch.Tensor", height: int, dist, rank: int, world: int, out=None):
+def gather_frame(buf: "torch.Tensor", height: int, dist, rank: int, world: int, out=None, host: bool = False):
     """The single collective of a step: dist.gather of every rank's row buffer to rank 0,
     straight into slices of one cached (N, rows_max, W, 3) staging tensor, then the
     un-permute into `out` (rank 0) as one strided copy.  Returns the frame on rank 0,
-    None elsewhere."""
+    None elsewhere.  host=True (gloo, whose collectives take host tensors): each rank's rows
+    go through host memory and rank 0 copies the assembled frame back into `out`."""
     import torch
 
+    if host and buf.is_cuda:
+        frame = gather_frame(buf.cpu(), height, dist, rank, world)
+        if rank != 0:
+            return None
+        if out is None:
+            return frame.to(buf.device)
+        out.copy_(frame)
+        return out
     if rank != 0:
         dist.gather(buf, gather_list=None, dst=0)
         return None

@@ -718,7 +718,8 @@ struct Sphere : Hitable {
     double radius;
     MatP material;
     AABB box;
-    Sphere(DVec3 c, double r, MatP m) : center(c), radius(r), material(std::move(m)) {
+    // SphereBuilder::build (sphere.rs:69-92): the box spans the centre at time 0 and 1
+    Sphere(DVec3 c, double r, MatP m, DVec3 s = {0, 0, 0}) : center(c), speed(s), radius(r), material(std::move(m)) {
         const DVec3 rvec{radius, radius, radius};
         const DVec3 c1 = center + speed;
         box = AABB::from_points(center - rvec, center + rvec).unite(AABB::from_points(c1 - rvec, c1 + rvec));
@@ -1109,7 +1110,8 @@ static Scene load_tree(const std::string& path) {
             const size_t id = U(t[1]);
             HitP p;
             const std::string& k = t[2];
-            if (k == "SPHERE") p = std::make_shared<Sphere>(F3(t, 3), F(t[6]), mat.at(U(t[7])));
+            if (k == "SPHERE")  // optional trailing speed (SphereBuilder::with_speed)
+                p = std::make_shared<Sphere>(F3(t, 3), F(t[6]), mat.at(U(t[7])), t.size() >= 11 ? F3(t, 8) : DVec3{0, 0, 0});
             else if (k == "QUAD" || k == "TRIANGLE") p = std::make_shared<Plane>(k == "QUAD", F3(t, 3), F3(t, 6), F3(t, 9), mat.at(U(t[12])));
             else if (k == "BVH") {
                 std::vector<HitP> list;

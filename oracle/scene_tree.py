@@ -11,7 +11,7 @@ Tree format (one item per line, floats as float.hex()):
     TEX id SOLID r g b | TEX id IMAGE w h <raw f32 file> | TEX id CHECKER even odd scale
     TEX id NOISE seed octaves frequency lacunarity persistence | TEX id MARBLE seed frequency
     MAT id LAMBERTIAN tex | METAL fuzz tex | DIELECTRIC ri | DIFFUSE_LIGHT intensity tex
-    OBJ id SPHERE c3 r mat | QUAD p3 u3 v3 mat | TRIANGLE p3 u3 v3 mat
+    OBJ id SPHERE c3 r mat [speed3] | QUAD p3 u3 v3 mat | TRIANGLE p3 u3 v3 mat
     OBJ id BVH n child... | TRANSLATE child o3 | ROTATE x|y|z child angle | SCALE child s3
     ROOT id
 

@@ -19,4 +19,6 @@ run c1_f32_big --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 &
 run c5_f32 && \
 run c5_f32_chacha --rng chacha8 && \
 run c5_f64_chacha --precision f64 --rng chacha8 --steps 1 && \
-run c5_f32_bvh --trace bvh
+run c5_f32_bvh --trace bvh && \
+{ timeout -k 10 200 python bench.py --cpu-only --scene scenes/spheres.toml --width 400 --height 225 --spp 16 --cpu-row-stride 1 > gpurun_out/${tag}_c1_cpu.json 2> gpurun_out/${tag}_c1_cpu.err && \
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('c1_cpu', d['value'], 'Msamples/s on', d['cpu_baseline']['cores'], 'cores')" gpurun_out/${tag}_c1_cpu.json; }

@@ -67,6 +67,39 @@ def test_shared_gpu_processes_bitwise_identical():
         np.testing.assert_array_equal(frame, want, err_msg=f"{p}/{r}")
 
 
+def _bench(n, extra=()):
+    """bench.py's own N-rank step (launched as the driver does, torch.distributed.run as a child
+    process) at a small size: its JSON line."""
+    import json
+    args = ["--gpus", str(n), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--width", "64", "--height", "37",
+            "--spp", "8", *extra]
+    bench = os.path.join(ROOT, "bench.py")
+    if n == 1:
+        cmd = [sys.executable, bench, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr=127.0.0.1", f"--master-port={_port()}", bench, *args]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("precision,rng", VARIANTS)
+def test_bench_multirank_step_matches_single(precision, rng):
+    """bench.py's N > 1 step (row shards, one gather to rank 0, un-permute, max-over-ranks timing)
+    runs end to end with two ranks sharing cuda:0 over gloo (the host-side gather; the RCCL
+    path is the same code with the collective on the device) and assembles the frame the
+    single-rank run renders, bit for bit (camera.rs:318-320: the RNG is keyed by pixel)."""
+    one = _bench(1, ("--precision", precision, "--rng", rng))
+    two = _bench(2, ("--precision", precision, "--rng", rng, "--backend", "gloo"))
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["value"] > 0 and two["ms_per_step"] > 0
+    assert one["frame_sha256"] and two["frame_sha256"] == one["frame_sha256"]
+
+
 def test_render_on_second_device_keeps_current_device():
     """The library renders on the scene's device whatever the caller's current device is,
     and leaves the caller's current device unchanged (device guard, render.hip)."""
