@@ -58,7 +58,7 @@ REC = {"f32": dict(node=32, prim=80, xform=112), "f64": dict(node=64, prim=144, 
 def scene_bytes(stats, precision):
     r = REC[precision]
     return (stats["nodes"] * r["node"] + stats["prims"] * r["prim"] + stats["xforms"] * r["xform"]
-            + stats["instances"] * 16 + stats["materials"] * 16 + stats["textures"] * 64 + stats["texels"] * 12)
+            + stats["instances"] * 16 + stats["materials"] * 16 + stats["textures"] * 64 + stats["texel_bytes"])
 
 
 # ------------------------------------------------------------------ CPU baseline

@@ -122,7 +122,7 @@ typedef struct {
 } nrt_render_opts;
 
 typedef struct {
-    uint64_t nodes, prims, instances, xforms, materials, textures, texels;
+    uint64_t nodes, prims, instances, xforms, materials, textures, texels; /* texels: of all image textures */
     uint32_t trees, max_instance_depth;
     uint64_t device_bytes; /* HBM bytes of the flattened scene on one device */
     uint64_t world_prims;  /* world-list test units after flattening instances to world space: primitives,
@@ -131,7 +131,7 @@ typedef struct {
     uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
                                 (else AUTO takes the world BVH, which compares tie keys) */
     uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
-    uint32_t reserved;
+    uint32_t texel_bytes;    /* HBM bytes of the texel array (RGBA8 images: 4 B per texel) */
 } nrt_scene_stats;
 /* Exact-kernel traversal (same closest hit and tie-break as BVH::hit, object.rs:89-121):
  *   BVH      the reference tree, box by box

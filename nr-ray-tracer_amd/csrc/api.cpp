@@ -221,9 +221,27 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     if (const char* e = std::getenv("NRT_EXACT_ALL")) p.exact_all = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.exact_wbvh = (!p.exact_all && mode == NRT_EXACT_WORLD) ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_WBVH")) p.exact_wbvh = std::strtol(e, nullptr, 10) != 0 && !f.wexact.empty();
+    // The world mode's f32 culling is conservative for ray origins near the scene: a slab end
+    // (f32, per-ray 1/d and o/d) moves the plane by at most ~2 ulp of (|origin| + |plane|), about
+    // 1.2e-7 (|origin| + scale), and the boxes are padded by 1e-6 scale (wbvh.cpp; scale = the
+    // largest |coordinate| of the primitives' boxes): safe for |origin| up to ~7 scale.  Secondary
+    // rays start on primitives; camera rays on the defocus disk around look_from: a camera beyond
+    // 4 scale takes the reference tree or the all-primitives walk instead (also over the knobs:
+    // a culled primitive would change the frame).
+    if (p.exact_wbvh) {
+        double ro = 0.0;
+        for (const double* v : {c.look_from, c.defocus_disk_u, c.defocus_disk_v})
+            ro += std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        if (!(ro <= 4.0 * f.exact_tree().scale)) {
+            p.exact_wbvh = 0;
+            p.exact_all = exact_walk_prims(f, f.root, EXACT_ALL_MAX) <= EXACT_ALL_MAX ? 1u : 0u;
+        }
+    }
     // plane-only scenes: the exact world mode's f32 prefilter (knob NRT_EXACT_PF=0 turns it off;
     // over every slot instead of the walk measured slower on Cornell, 223 against 217 ms)
     p.exact_pf = 1;
+    p.exact_thread = 1;  // knob NRT_EXACT_THREAD=0: the 4-wide stack walk (round 2)
+    if (const char* e = std::getenv("NRT_EXACT_THREAD")) p.exact_thread = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
@@ -233,6 +251,14 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // knob NRT_WAVE_PIXELS (a power of two 1..128).  ChaCha8 streams are sequential:
     // one lane per pixel.
     p.wave_pixels = 1;
+    // Philox group distribution: 90 % of each eighth's groups statically, round-robin over the
+    // waves of its label, the rest through the per-label queue head (one device-scope atomic per
+    // group: those run at the memory side, ~32 B of HBM writes each); knob NRT_STATIC_SHARE 0..1024
+    p.static_share = 922;
+    if (const char* e = std::getenv("NRT_STATIC_SHARE")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 0 && v <= 1024) p.static_share = (uint32_t)v;
+    }
     if (o && o->rng == NRT_RNG_PHILOX) {
         p.wave_pixels = 0;
         if (const char* e = std::getenv("NRT_WAVE_PIXELS")) {
@@ -564,14 +590,14 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
         out->xforms = f.xforms.size();
         out->materials = f.materials.size();
         out->textures = f.textures.size();
-        out->texels = f.texels.size() / 3;
+        out->texels = f.texel_count;
         out->trees = f.num_trees;
         out->max_instance_depth = (uint32_t)f.max_depth;
         out->device_bytes = f.nodes.size() * (sizeof(DNode<double>) + sizeof(DNode<float>)) +
                             f.prims.size() * (sizeof(DPrim<double>) + sizeof(DPrim<float>)) +
                             f.xforms.size() * (sizeof(DXform<double>) + sizeof(DXform<float>)) +
                             f.instances.size() * sizeof(DInstance) + f.materials.size() * sizeof(DMaterial) +
-                            f.textures.size() * sizeof(DTexture) + f.texels.size() * sizeof(float) +
+                            f.textures.size() * sizeof(DTexture) + f.texels.size() * sizeof(uint32_t) +
                             f.nodes_fast.size() * sizeof(DNode<float>) + f.fprims.size() * sizeof(DPrimFast<float>) +
                             f.inst_fast.size() * sizeof(DInstFast<float>) + f.mats_fast.size() * sizeof(DMatFast) +
                             f.wprims.size() * sizeof(DPrimWorld<float>);
@@ -579,7 +605,7 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
         out->coplanar_pairs = f.coplanar_pairs;
         out->world_list_ok = f.world_ok && f.list_ok ? 1u : 0u;
         out->exact_mode = exact_mode(f);
-        out->reserved = 0;
+        out->texel_bytes = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, f.texels.size() * sizeof(uint32_t));
         return NRT_OK;
     });
 }

@@ -95,9 +95,10 @@ struct alignas(16) DPrimWorld {
     Real D;         // plane: d - n.b                sphere: radius
     // plane: (A.x, B.x, A.y, B.y, A.z, B.z, a0', b0') with A = M^T (v x w),
     // B = M^T (w x u), a0' = a0 - (v x w).b, b0' = b0 - (w x u).b: pairs, so the
-    // kernel gets (alpha, beta) from packed FMAs;   sphere: speed in [0..2]
+    // kernel gets (alpha, beta) from packed FMAs;   sphere: speed in [0..2], P in [3..5] = the
+    // point of the sphere (at time 0) nearest the world origin, [6] = 1 when tested in f64
     Real AB[8];
-    Real S[3];      // plane: shading normal (rotations of the chain applied to n)
+    Real S[3];      // plane: shading normal (rotations of the chain applied to n)   sphere: V = P - center
     uint32_t meta;  // kind | material << 2
 };
 // PRIM_QUAD_X/Y/Z (world list): the plane is x_a = P with a = kind - PRIM_QUAD_X;
@@ -115,6 +116,9 @@ struct alignas(16) DPrimWorld {
 // lies on plane l_axis = D + side * L.  The quads keep their own records (uv,
 // normals, material) for the hit record.
 constexpr uint32_t BOX_ENTRIES = 7;
+// f32 kernels test a sphere in f32 when |center| + |speed| + |r| stays within this (kernel.hpp
+// sphere_t_world), else in f64
+constexpr double SPHERE_F32_EXTENT = 100.0;
 // PRIM_BOXY (world-list run kind only; header meta kind stays PRIM_BOX): a box turned
 // about the world y axis only.  Local axes (A, y, B): (N[0], N[2], D) = x, z entries
 // of row A and its offset, (AB[0], AB[2], AB[3]) the same for row B (their y entries
@@ -168,7 +172,9 @@ struct alignas(16) DBvhNode {
 // child boxes quantized to 8 bits per plane relative to the node's box,
 // lo_k = org + qlo_k * 2^(e - 127) per axis, rounded outward on the host (the
 // decoded box always contains the f32 child box).  Traversal is gather-bound
-// (each lane loads a different node), so bytes per visit set the speed.
+// (each lane loads a different node), so bytes per visit set the speed: a 128-byte
+// node with the child planes in f32 (no decode, 40 % fewer VALU instructions per visit)
+// measured 20 % slower on the teapot (C4 40.3 -> 48.5 ms, round 3).
 struct alignas(16) DBvh4Node {
     float org[3];      // lower corner of the node's box
     uint32_t exps;     // scale exponent byte per axis (bits 0-7 x, 8-15 y, 16-23 z)
@@ -178,10 +184,43 @@ struct alignas(16) DBvh4Node {
     uint32_t pad[2];
 };
 static_assert(sizeof(DBvh4Node) == 64, "one half cache line per 4-wide node");
+// Compact 4-wide node, 48 bytes (three 16-byte loads per visit instead of four): the 64-byte
+// node's quantized boxes with 16-bit child refs.  The teapot's traversal is bound by the
+// vector memory path (L1 accesses: one per lane and load instruction), so a load less per
+// visit is a quarter of the node traffic.  Built when every leaf holds at most 4 primitives,
+// the tree has < 32768 nodes and < 8192 primitive slots (wbvh.cpp); the scene-specialised
+// world-BVH kernel reads it (BvhSig width WBVH_COMPACT), with a 16-bit LDS stack.
+struct alignas(16) DBvh4cNode {
+    float org[3];
+    uint32_t exps;
+    uint32_t qlo[3];
+    uint32_t qhi[3];
+    uint16_t child[4];  // leaf: WBVH4C_LEAF | first << 2 | (count - 1); inner: node index
+};
+static_assert(sizeof(DBvh4cNode) == 48, "three 16-byte loads per compact 4-wide node");
+constexpr uint32_t WBVH4C_LEAF = 0x8000u, WBVH4C_LEAF_MAX = 4, WBVH4C_MAX_PRIMS = 8192, WBVH4C_MAX_NODES = 32768;
+constexpr int WBVH_COMPACT = 5;  // BvhSig width code of the compact 4-wide tree
+// primitive kinds of a world BVH's leaves (the scene-specialised kernel's BvhSig)
+enum : int { WPRIMS_ANY = 0, WPRIMS_TRIANGLES = 1, WPRIMS_QUADS = 2 };
 constexpr int32_t WBVH_DONE = INT32_MIN;  // "stack empty" marker (never a valid leaf ref)
 constexpr int32_t WBVH_NO_LEAF = 0;       // "no parked leaf" (leaf refs are negative)
 constexpr uint32_t WBVH_STACK = 32;       // per-lane stack entries at most (host checks the tree's bound)
 constexpr uint32_t WBVH_LEAF_MAX = 8;
+
+// Exact kernel's culling walk without a stack: the binary world BVH threaded in depth-first
+// order, one copy per ray-direction octant (bit 0: d.x < 0, bit 1: d.y < 0, bit 2: d.z < 0) in
+// which every node's nearer child (box centres along the octant's diagonal) comes first and the
+// box planes are stored as (near, far) for that octant's signs.  A hit node continues at the
+// next record (its first child, or past a leaf's primitives at skip), a missed one at skip,
+// the subtree's end: no stack, so no scratch traffic (round 2's private-array stack and the
+// spills around it wrote 8.7 GB per C5 launch), and the walk keeps near-first order.
+struct alignas(16) DThreadNode {
+    float nearp[3];  // the box planes the octant's rays enter through (lo for d >= 0, else hi)
+    int32_t skip;    // index (within the octant's copy) of the record after this subtree
+    float farp[3];
+    int32_t leaf;    // leaf ref ~(first << 3 | count - 1), 0 for an inner node
+};
+static_assert(sizeof(DThreadNode) == 32, "two 16-byte loads per threaded node");
 
 // Exact kernel over the world BVH (RenderParams::exact_wbvh): for each BVH primitive slot,
 // the reference primitive it is (DPrim index), the instance whose Translate/Rotate/Scale
@@ -239,12 +278,31 @@ struct alignas(16) DMatFast {
     float pad;
 };
 
+// Image texel formats in the texel array (32-bit words): RGBA8 = one word per texel, bytes
+// r | g << 8 | b << 16, for images whose every value is k / 255 (every image a file gives:
+// into_rgb32f, textures/image.rs:24-28; the kernel rebuilds k / 255.0f exactly); RGB32F =
+// three f32 words per texel (images from the constructor API with other values).
+// RGBA8 images are stored in tiles of 8 x 4 texels (128 bytes, one cache line), tiles in rows
+// of ceil(W / 8): rays that hit nearby points of a sphere read nearby texels in both directions,
+// so a line fetched for one serves its neighbours above and below as well (earth.toml: 4.96 GB
+// of HBM/MALL fetches per C3 launch with f32 row-major texels).
+enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1 };
+#if defined(__HIPCC_RTC__)
+#define NRT_HD __device__
+#elif defined(__HIPCC__)
+#define NRT_HD __host__ __device__
+#else
+#define NRT_HD
+#endif
+NRT_HD inline uint64_t tex_tiled_index(uint32_t x, uint32_t y, uint32_t tiles_per_row) {
+    return ((uint64_t)(y >> 2) * tiles_per_row + (x >> 3)) * 32u + (y & 3u) * 8u + (x & 7u);
+}
 struct alignas(16) DTexture {
     uint32_t kind;
     uint32_t a, b;     // image: width, height; checker: even, odd texture ids; noise/marble: octaves, seed
-    uint32_t pad;
-    uint64_t offset;   // image: first texel (float index / 3) in the texel array; noise/marble: first
-                       // permutation table (octaves x 256 floats 0..255) likewise
+    uint32_t format;   // image: TEXFMT_*
+    uint64_t offset;   // image: first word of its texels in the texel array; noise/marble: first word of
+                       // its permutation tables (octaves x 256 words, values 0..255)
     double color[3];   // solid colour; noise/marble: frequency, lacunarity, persistence
     double scale;      // checker scale; noise/marble: Fbm scale factor
 };
@@ -258,7 +316,7 @@ struct DSceneView {
     const DInstance* instances;
     const DMaterial* materials;
     const DTexture* textures;
-    const float* texels;
+    const uint32_t* texels;  // image texels (TEXFMT_*) and Perlin permutation tables, 32-bit words
     int32_t root;
     int32_t max_depth;  // deepest instance nesting (0 = no instances)
     uint32_t n_nodes, n_prims, n_xforms, n_instances, n_materials, n_textures;
@@ -273,6 +331,7 @@ struct DSceneView {
     uint32_t wflags;                 // WFLAG_*: what the world list holds
     const DBvhNode* wbvh;            // world-BVH mode: nodes (wprims then holds the BVH-ordered prims)
     const DBvh4Node* wbvh4;          // the same tree collapsed to 4-wide nodes (root = wbvh4_root)
+    const DBvh4cNode* wbvh4c;        // ... in the compact 48-byte form (same indices and root), or null
     int32_t wbvh4_root;
     int32_t wbvh_root;               // child ref of the root
     uint32_t n_wbvh;
@@ -280,6 +339,8 @@ struct DSceneView {
     // allocate that many + 1 (branch-free pushes) in LDS, so shallow trees leave room for
     // more workgroups per CU
     uint32_t wbvh_stack;
+    const DThreadNode* xthread;  // f64 view: the culling tree threaded per octant (8 copies of n_xthread)
+    uint32_t n_xthread;
     const DExactRef* wexact;  // f64 view: exact reference of each world-BVH slot (exact_wbvh mode)
     const DPrimWorld<float>* wxprims;  // f64 view: f32 world primitive of each of those slots (prefilter)
     uint32_t n_wexact;                 // slots of that tree

@@ -3,6 +3,7 @@
 
 #include <climits>
 #include <cmath>
+#include <cstring>
 #include <cstdlib>
 #include <cstdint>
 #include <cstdio>
@@ -44,13 +45,45 @@ struct Flattener {
                 d.kind = TEX_SOLID;
                 d.color[0] = t->color.x; d.color[1] = t->color.y; d.color[2] = t->color.z;
                 break;
-            case Texture::Image:
+            case Texture::Image: {
                 d.kind = TEX_IMAGE;
                 d.a = t->width;
                 d.b = t->height;
-                d.offset = out.texels.size() / 3;
-                out.texels.insert(out.texels.end(), t->texels->begin(), t->texels->end());
+                d.offset = out.texels.size();
+                out.texel_count += (uint64_t)t->width * t->height;
+                // RGBA8 when every value is k / 255 in f32 (files always are: into_rgb32f), else RGB32F
+                const std::vector<float>& px = *t->texels;
+                bool unorm8 = true;
+                for (size_t i = 0; i < px.size() && unorm8; ++i) {
+                    const float v = px[i];
+                    const float k = std::nearbyint(v * 255.0f);
+                    unorm8 = k >= 0.0f && k <= 255.0f && (float)k / 255.0f == v && !std::signbit(v);
+                }
+                d.format = unorm8 ? TEXFMT_RGBA8 : TEXFMT_RGB32F;
+                if (unorm8) {  // 8 x 4 texel tiles of one 128-byte line each, rows of tiles (tex_texel_index)
+                    const uint32_t tw = (t->width + 7u) / 8u, th = (t->height + 3u) / 4u;
+                    const size_t base = out.texels.size();
+                    out.texels.resize(base + (size_t)tw * th * 32u, 0u);
+                    for (uint32_t y = 0; y < t->height; ++y)
+                        for (uint32_t x = 0; x < t->width; ++x) {
+                            const float* v = px.data() + 3ull * ((size_t)y * t->width + x);
+                            uint32_t w = 0;
+                            for (int c = 0; c < 3; ++c) w |= (uint32_t)std::nearbyint(v[c] * 255.0f) << (8 * c);
+#ifdef NRT_TEX_ROWMAJOR  // (A/B build: row-major RGBA8)
+                            out.texels[base + (size_t)y * t->width + x] = w;
+#else
+                            out.texels[base + tex_tiled_index(x, y, tw)] = w;
+#endif
+                        }
+                } else {
+                    for (float v : px) {
+                        uint32_t w;
+                        std::memcpy(&w, &v, 4);
+                        out.texels.push_back(w);
+                    }
+                }
                 break;
+            }
             case Texture::Checker: {
                 d.kind = TEX_CHECKER;
                 d.scale = t->scale;
@@ -62,7 +95,7 @@ struct Flattener {
             case Texture::Noise:
             case Texture::Marble: {
                 // Abs<Fbm<Perlin>>: one permutation table per octave (seed + k), stored
-                // in the texel array as floats 0..255 (exact), starting on a triplet
+                // in the texel array, one word per entry
                 d.kind = t->kind == Texture::Noise ? TEX_NOISE : TEX_MARBLE;
                 const FbmParams& f = t->fbm;
                 d.a = f.octaves;
@@ -71,14 +104,12 @@ struct Flattener {
                 d.color[1] = f.lacunarity;
                 d.color[2] = f.persistence;
                 d.scale = fbm_scale_factor(f.persistence, f.octaves);
-                while (out.texels.size() % 3) out.texels.push_back(0.f);
-                d.offset = out.texels.size() / 3;
+                d.offset = out.texels.size();
                 uint8_t perm[256];
                 for (uint32_t k = 0; k < f.octaves; ++k) {
                     perlin_permutation(f.seed + k, perm);  // Fbm build_sources: seed + k (u32 wrap)
-                    for (int i = 0; i < 256; ++i) out.texels.push_back((float)perm[i]);
+                    for (int i = 0; i < 256; ++i) out.texels.push_back(perm[i]);
                 }
-                while (out.texels.size() % 3) out.texels.push_back(0.f);
                 break;
             }
         }
@@ -776,6 +807,22 @@ struct Flattener {
                 const V3a c = va(o->center);
                 for (int k = 0; k < 3; ++k) { w.N[k] = c[k] - f.b[k]; w.AB[k] = va(o->speed)[k]; }
                 w.D = o->radius;
+                // f32 kernels (kernel.hpp sphere_t_world): the point P of the sphere (at time 0)
+                // nearest the world origin in AB[3..5] and V = P - center in S, in f64 here
+                const double cl = std::sqrt(w.N[0] * w.N[0] + w.N[1] * w.N[1] + w.N[2] * w.N[2]);
+                const double ar = std::fabs(o->radius);
+                for (int k = 0; k < 3; ++k) {
+                    const double u = cl > 0.0 ? -w.N[k] / cl : (k == 1 ? -1.0 : 0.0);  // toward the origin
+                    w.S[k] = ar * u;
+                    w.AB[3 + k] = w.N[k] + ar * u;
+                }
+                // AB[6] = 1: tested in f64 (spheres larger than the scene scale)
+                const double sl = std::sqrt(w.AB[0] * w.AB[0] + w.AB[1] * w.AB[1] + w.AB[2] * w.AB[2]);
+                static const bool f32_ok = [] {  // knob NRT_SPHERE_F32=0: every sphere in f64 (A/B runs)
+                    const char* e = std::getenv("NRT_SPHERE_F32");
+                    return !(e && e[0] == '0');
+                }();
+                w.AB[6] = f32_ok && cl + sl + ar <= SPHERE_F32_EXTENT ? 0.0 : 1.0;
                 const uint32_t mat = material(o->material);
                 if (mat > WMAT_MASK) { out.world_ok = false; return; }
                 w.meta = PRIM_SPHERE | (mat << WKIND_BITS);
@@ -872,7 +919,14 @@ struct Flattener {
             for (int k = 0; k < 3; ++k) { bounds[i][k] = lo[k]; bounds[i][3 + k] = hi[k]; }
         }
         try {
-            out.wbvh = build_world_bvh(bounds, cost);
+            // leaves of at most WBVH4C_LEAF_MAX primitives where the compact 4-wide form can hold the
+            // tree (DBvh4cNode; knob NRT_WBVH_LEAF = 1..8 for A/B runs)
+            uint32_t leaf_max = out.wprims.size() < WBVH4C_MAX_PRIMS ? WBVH4C_LEAF_MAX : WBVH_LEAF_MAX;
+            if (const char* e = std::getenv("NRT_WBVH_LEAF")) {
+                const long v = std::strtol(e, nullptr, 10);
+                if (v >= 1 && v <= (long)WBVH_LEAF_MAX) leaf_max = (uint32_t)v;
+            }
+            out.wbvh = build_world_bvh(bounds, cost, leaf_max);
         } catch (const std::runtime_error&) {
             out.wbvh_ok = false;
             return;

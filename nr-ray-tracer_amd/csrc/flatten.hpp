@@ -22,7 +22,8 @@ struct FlatScene {
     std::vector<DInstance> instances;
     std::vector<DMaterial> materials;
     std::vector<DTexture> textures;
-    std::vector<float> texels;
+    std::vector<uint32_t> texels;  // 32-bit words (device_scene.hpp DTexture: TEXFMT_*, permutation tables)
+    uint64_t texel_count = 0;       // image texels over all image textures
     int32_t root = NODE_END;
     int32_t max_depth = 0;
     uint32_t num_trees = 0;

@@ -534,6 +534,44 @@ __device__ __forceinline__ R fast_prim_t(const DPrimFast<R>& q, const Ray<R>& r,
     return ok ? t : R(-1);
 }
 
+// Sphere::hit root selection (sphere.rs:105-163) in f32 for the world modes (the
+// r = 1e5 and r = 1e3 ground spheres).  Relative to P, the sphere's point nearest the world
+// origin (host, f64; moving with the centre), and V = P - center (|V| = |r|), with e = o - P:
+//   c = |o - center|^2 - r^2 = |e|^2 + 2 e.V     (no |center|^2 - r^2 cancellation: a ground
+//                                                 sphere's P is at the scene, e stays small)
+//   h = (center - o).d = -(e.d + V.d)
+// and the root nearer zero as c / q with q = h + sign(h) sqrt(h^2 - a c) (Press et al.): no
+// cancellation for the self-intersection root of a ray leaving the surface.  Returns the
+// smaller root in (0.001, inf), else the larger, else -1, as the reference.
+template <class Q>  // Q: a DPrimWorld<float> in any address space (world list: the constant one)
+__device__ __forceinline__ float sphere_t_world_f32(const Q& q, const Ray<float>& r) {
+    const V<float> P = mk(q.AB[3], q.AB[4], q.AB[5]) + r.time * mk(q.AB[0], q.AB[1], q.AB[2]);
+    const V<float> v = mk(q.S[0], q.S[1], q.S[2]);
+    const V<float> e = r.o - P;
+    const float a = dot(r.d, r.d);
+    const float h = -(dot(e, r.d) + dot(v, r.d));
+    const float c = dot(e, e) + 2.0f * dot(e, v);
+    const float disc = h * h - a * c;
+    const float qq = h + __builtin_copysignf(__builtin_amdgcn_sqrtf(fmaxf(disc, 0.0f)), h);
+    const float t1 = qq * __builtin_amdgcn_rcpf(a), t2 = c * __builtin_amdgcn_rcpf(qq);
+    const float tn = fminf(t1, t2), tf = fmaxf(t1, t2);
+    const float t = tn > 0.001f ? tn : tf;
+    return ((disc >= 0.0f) & (t > 0.001f) & (t < INFINITY)) ? t : -1.0f;
+}
+// The world modes' sphere test: f32 (above) for spheres within the scene's scale (AB[6] = 0:
+// |center| + |speed| + |r| <= SPHERE_F32_EXTENT, flatten.cpp), whose hit points the record then
+// puts back on the surface (make_record_world); the quadratic in f64 for the large ones (the
+// r = 1e5 and r = 1e3 ground spheres): their f32 hit points would sit up to ~1e-5 off a surface
+// of that size, and the next ray's t_min = 0.001 would not hide the self-intersection.
+template <class Q>
+__device__ __forceinline__ float sphere_t_world(const Q& q, const Ray<float>& r) {
+    if (q.AB[6] == 0.0f) return sphere_t_world_f32(q, r);
+    DPrim<float> sp;
+    for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
+    sp.s = q.D;
+    return sphere_t(sp, r);  // (f32 specialisation: in f64)
+}
+
 // ray into object space through an instance's chain (outer -> inner)
 template <typename R, bool EXACT, bool PREP = true>  // PREP: 1/d for slab tests (not needed by prim tests)
 __device__ __forceinline__ void xform_in(const DSceneView<R>& sc, const DInstance& inst, Ray<R>& r) {
@@ -758,10 +796,7 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
     }
     if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres (not compiled in)
         for (; k < end; ++k) {
-            DPrim<float> sp;
-            for (int c = 0; c < 3; ++c) { sp.a[c] = wp[k].N[c]; sp.b[c] = wp[k].AB[c]; }
-            sp.s = wp[k].D;
-            const float t = sphere_t(sp, ray);
+            const float t = sphere_t_world(wp[k], ray);
             const bool ok = (t >= 0.0f) & (t <= t_best);
             t_best = ok ? t : t_best;
             best = ok ? (int32_t)k : best;
@@ -793,6 +828,7 @@ struct NoSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = 0;  // world-BVH width known at compile time (BvhSig), 0: read sc.wbvh4
     static constexpr bool tie = false;
+    static constexpr int prims = 0;  // world-BVH leaf primitive kinds (WPRIMS_*), 0: decided per primitive
     static constexpr int exact = 0;  // exact kernel: traversal fixed at compile time (ExactSig), 0: runtime
 };
 template <uint32_t... RUNS>
@@ -800,6 +836,7 @@ struct WorldSig {
     static constexpr uint32_t n = sizeof...(RUNS);
     static constexpr int bvh = 0;
     static constexpr bool tie = false;
+    static constexpr int prims = 0;
     static constexpr int exact = 0;
 };
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
@@ -809,17 +846,21 @@ enum : int { EXACT_SIG_WORLD_PF = 1 };
 template <int MODE, int WIDTH>
 struct ExactSig {
     static constexpr uint32_t n = 0;
-    static constexpr int bvh = WIDTH;  // the culling tree's width (2 or 4), 0: sc.wbvh4 at run time
+    static constexpr int bvh = WIDTH;  // culling walk: 4 / 2 the stack walk of that width, XTHREAD_W the
+                                       // threaded tree, 0: chosen at run time
     static constexpr bool tie = false;
+    static constexpr int prims = 0;
     static constexpr int exact = MODE;
 };
-// World-BVH mode (jit.hip): the tree's width (2 or 4) and whether it holds coplanar-tie
-// keys (WFLAG_COPLANAR) as constants, so one traversal variant is compiled instead of four.
-template <int WIDTH, bool TIE>
+// World-BVH mode (jit.hip): the tree's width (2 or 4), whether it holds coplanar-tie keys
+// (WFLAG_COPLANAR) and which primitive kinds its leaves hold (WPRIMS_*) as constants, so one
+// traversal and one primitive test are compiled instead of several.
+template <int WIDTH, bool TIE, int PRIMS = WPRIMS_ANY>
 struct BvhSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = WIDTH;
     static constexpr bool tie = TIE;
+    static constexpr int prims = PRIMS;
     static constexpr int exact = 0;
 };
 template <bool FLAT, uint32_t... RUNS>
@@ -876,14 +917,11 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
 // lane's stack (LDS, entry k at stack[k * BLOCK]), so t_best shrinks early and
 // culls the far side.  The lanes of a wave descend until each holds a leaf (or
 // is done) before leaves are tested together ("while-while").
-template <bool FLAT = false, bool TIE = false>
+template <bool FLAT = false, bool TIE = false, int PRIMS = 0>  // PRIMS: WPRIMS_* of the scene's leaves
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
     const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
     if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres
-        DPrim<float> sp;
-        for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
-        sp.s = q.D;
-        const float t = sphere_t(sp, ray);
+        const float t = sphere_t_world(q, ray);
         return (t >= 0.0f && t <= t_best) ? t : -1.0f;
     }
     const V<float> nrm = ld3(q.N);
@@ -893,8 +931,8 @@ __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const 
     const float alpha = dot(pt, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
     const float beta = dot(pt, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
     const float lo = fminf(alpha, beta);
-    const bool inside = kind == PRIM_QUAD ? (lo >= 0.0f) & (alpha <= 1.0f) & (beta <= 1.0f)
-                                          : (lo > 0.0f) & (alpha + beta < 1.0f);
+    const bool quad = PRIMS == 1 ? false : (PRIMS == 2 ? true : kind == PRIM_QUAD);
+    const bool inside = quad ? (lo >= 0.0f) & (alpha <= 1.0f) & (beta <= 1.0f) : (lo > 0.0f) & (alpha + beta < 1.0f);
     const float key = tie_key<TIE>(t, tie_factor(q.meta >> WCLASS_SHIFT));  // coplanar-tie key
     const bool ok = (fabsf(denom) >= 1e-8f) & (t >= 0.001f) & (key <= t_best) & inside;
     return ok ? key : -1.0f;
@@ -986,6 +1024,9 @@ struct PrivStack {
 };
 __device__ __forceinline__ void stk_write(int32_t* s, uint32_t k, int32_t v) { s[k * BLOCK] = v; }
 __device__ __forceinline__ int32_t stk_read(int32_t* s, uint32_t k) { return s[k * BLOCK]; }
+// compact 4-wide tree (BvhSig width WBVH_COMPACT): the raw 16-bit child refs
+__device__ __forceinline__ void stk_write(uint16_t* s, uint32_t k, int32_t v) { s[k * BLOCK] = (uint16_t)v; }
+__device__ __forceinline__ int32_t stk_read(uint16_t* s, uint32_t k) { return (int32_t)s[k * BLOCK]; }
 __device__ __forceinline__ void stk_write(PrivStack& s, uint32_t k, int32_t v) { s.e[k] = v; }
 __device__ __forceinline__ int32_t stk_read(PrivStack& s, uint32_t k) { return s.e[k]; }
 template <class STK>
@@ -1078,26 +1119,83 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
     t.node = t0 != INFINITY ? c0 : wbvh_pop(t, stack);
 }
 
+// Compact 4-wide visit (DBvh4cNode: the same boxes, 16-bit child refs; three loads instead of
+// four).  The stack holds the raw 16-bit refs; a ref becomes the traversal's 32-bit form
+// (inner index, or ~(first << 3 | count - 1) for a leaf) only when it is taken (wbvh4c_ref).
+__device__ __forceinline__ int32_t wbvh4c_ref(uint32_t r) {
+    return (r & WBVH4C_LEAF) ? ~(int32_t)(((r & 0x7FFCu) << 1) | (r & 3u)) : (int32_t)r;
+}
+template <class STK>
+__device__ __forceinline__ int32_t wbvh4c_pop(WbvhTrav& ts, STK& stack) {
+    return ts.sp ? wbvh4c_ref((uint32_t)stk_read(stack, --ts.sp)) : WBVH_DONE;
+}
+template <typename R, class STK>
+__device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
+    const DBvh4cNode nd = load16(sc.wbvh4c + t.node);
+    const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
+    const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
+    const float Az = __uint_as_float(((nd.exps >> 16) & 0xFFu) << 23) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
+    const bool px = t.ix >= 0.0f, py = t.iy >= 0.0f, pz = t.iz >= 0.0f;
+    const uint32_t nqx = px ? nd.qlo[0] : nd.qhi[0], fqx = px ? nd.qhi[0] : nd.qlo[0];
+    const uint32_t nqy = py ? nd.qlo[1] : nd.qhi[1], fqy = py ? nd.qhi[1] : nd.qlo[1];
+    const uint32_t nqz = pz ? nd.qlo[2] : nd.qhi[2], fqz = pz ? nd.qhi[2] : nd.qlo[2];
+    auto child_t = [&](int k) {  // entry distance of child k, +inf if missed or empty
+        auto q = [&](uint32_t w) { return (float)((w >> (8 * k)) & 0xFFu); };
+        const float nx = q(nqx) * Ax + Bx, fx = q(fqx) * Ax + Bx;
+        const float ny = q(nqy) * Ay + By, fy = q(fqy) * Ay + By;
+        const float nz = q(nqz) * Az + Bz, fz = q(fqz) * Az + Bz;
+        const float n = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.0f));
+        const float f = fminf(fminf(fx, fy), fminf(fz, t.t_best));
+        return n <= f ? n : INFINITY;
+    };
+    float t0 = child_t(0), t1 = child_t(1), t2 = child_t(2), t3 = child_t(3);
+    const uint32_t c01 = (uint32_t)nd.child[0] | ((uint32_t)nd.child[1] << 16);
+    const uint32_t c23 = (uint32_t)nd.child[2] | ((uint32_t)nd.child[3] << 16);
+    int32_t c0 = (int32_t)(c01 & 0xFFFFu), c1 = (int32_t)(c01 >> 16), c2 = (int32_t)(c23 & 0xFFFFu),
+            c3 = (int32_t)(c23 >> 16);
+    wbvh_cswap(t0, c0, t1, c1);  // nearest hit child first; the others keep their slots
+    wbvh_cswap(t0, c0, t2, c2);
+    wbvh_cswap(t0, c0, t3, c3);
+    stk_write(stack, t.sp, c3);
+    t.sp += t3 != INFINITY ? 1u : 0u;
+    stk_write(stack, t.sp, c2);
+    t.sp += t2 != INFINITY ? 1u : 0u;
+    stk_write(stack, t.sp, c1);
+    t.sp += t1 != INFINITY ? 1u : 0u;
+    t.node = t0 != INFINITY ? wbvh4c_ref((uint32_t)c0) : wbvh4c_pop(t, stack);
+}
+// Visit / pop of a tree of width W (2 binary, 4 four-wide, WBVH_COMPACT the compact four-wide)
+template <int W, typename R, class STK>
+__device__ __forceinline__ void wbvh_visit_w(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
+    if constexpr (W == WBVH_COMPACT) wbvh4c_visit(t, sc, stack);
+    else if constexpr (W == 4) wbvh4_visit(t, sc, stack);
+    else wbvh2_visit(t, sc, stack);
+}
+template <int W, class STK>
+__device__ __forceinline__ int32_t wbvh_pop_w(WbvhTrav& ts, STK& stack) {
+    if constexpr (W == WBVH_COMPACT) return wbvh4c_pop(ts, stack);
+    else return wbvh_pop(ts, stack);
+}
+
 // One round: descend through inner nodes until the lane holds a leaf (or is
 // done), lanes waiting for the wave's slowest; then test the leaf.  With
 // NRT_SPECULATIVE (Aila & Laine) a lane that meets a leaf parks it and keeps
 // descending until every lane of the wave has a leaf.
-template <typename R, bool WIDE, bool FLAT>
+template <typename R, int W, bool FLAT, class STKP>
 __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                                int32_t* stack, unsigned long long* pc) {
+                                                STKP stack, unsigned long long* pc) {
 #if NRT_SPECULATIVE
     while (true) {
         if (ts.node < 0 && ts.node != WBVH_DONE && ts.leaf == WBVH_NO_LEAF) {  // park a leaf
             ts.leaf = ts.node;
-            ts.node = wbvh_pop(ts, stack);
+            ts.node = wbvh_pop_w<W>(ts, stack);
         }
         const bool inner = ts.node >= 0;
         if (!__any(inner)) break;                                         // nobody can descend
         if (__all(ts.leaf != WBVH_NO_LEAF || ts.node == WBVH_DONE)) break;  // every lane has a leaf (or is done)
         if (inner) {
             prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
-            if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
-            else wbvh2_visit(ts, sc, stack);
+            wbvh_visit_w<W>(ts, sc, stack);
         }
     }
     if (ts.leaf != WBVH_NO_LEAF) {
@@ -1105,13 +1203,10 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
         ts.leaf = WBVH_NO_LEAF;
     }
 #else
-    while (ts.node >= 0) {
-        if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
-        else wbvh2_visit(ts, sc, stack);
-    }
+    while (ts.node >= 0) wbvh_visit_w<W>(ts, sc, stack);
     if (ts.node == WBVH_DONE) return;
     wbvh_leaf<R, FLAT>(ts, sc, ray, ts.node);
-    ts.node = wbvh_pop(ts, stack);
+    ts.node = wbvh_pop_w<W>(ts, stack);
 #endif
 }
 
@@ -1120,44 +1215,43 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
 // or a pop turns up becomes the lane's leaf cursor at once (the leaf ref, advanced in place:
 // first + 1, count - 1).  Lanes never wait for the wave to finish a phase, so long and
 // short traversals, and leaves of different sizes, interleave across trips.
-template <typename R, bool WIDE, bool FLAT, bool TIE>
+template <typename R, int W, bool FLAT, bool TIE, int PRIMS = 0, class STKP>
 __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                               int32_t* stack, unsigned long long* pc) {
+                                               STKP stack, unsigned long long* pc) {
     if (ts.leaf != WBVH_NO_LEAF) {
         prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
         const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
         const DPrimWorld<float> q = load16(sc.wprims + first);
-        const float t = world_prim_t<FLAT, TIE>(q, ray, ts.t_best);
+        const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
         const bool ok = t >= 0.0f;
         ts.t_best = ok ? t : ts.t_best;
         ts.best = ok ? (int32_t)first : ts.best;
         ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
     } else if (ts.node >= 0) {
         prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
-        if constexpr (WIDE) wbvh4_visit(ts, sc, stack);
-        else wbvh2_visit(ts, sc, stack);
+        wbvh_visit_w<W>(ts, sc, stack);
     }
     if (ts.leaf == WBVH_NO_LEAF && ts.node < 0 && ts.node != WBVH_DONE) {  // a leaf turned up: its cursor
         ts.leaf = ts.node;
-        ts.node = wbvh_pop(ts, stack);
+        ts.node = wbvh_pop_w<W>(ts, stack);
     }
 }
-template <typename R, bool WIDE, bool FLAT>
+template <typename R, int W, bool FLAT, class STKP>
 __device__ __forceinline__ void wbvh_trip(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                          int32_t* stack, unsigned long long* pc) {
-    if (sc.wflags & WFLAG_COPLANAR) wbvh_trip_impl<R, WIDE, FLAT, true>(ts, sc, ray, stack, pc);
-    else wbvh_trip_impl<R, WIDE, FLAT, false>(ts, sc, ray, stack, pc);
+                                          STKP stack, unsigned long long* pc) {
+    if (sc.wflags & WFLAG_COPLANAR) wbvh_trip_impl<R, W, FLAT, true>(ts, sc, ray, stack, pc);
+    else wbvh_trip_impl<R, W, FLAT, false>(ts, sc, ray, stack, pc);
 }
 
-template <typename R, bool FLAT = false>
+template <typename R, bool FLAT = false, class STKP>
 __device__ __forceinline__ void wbvh_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                           int32_t* stack, unsigned long long* pc) {
-    wbvh_round_impl<R, false, FLAT>(ts, sc, ray, stack, pc);
+                                           STKP stack, unsigned long long* pc) {
+    wbvh_round_impl<R, 2, FLAT>(ts, sc, ray, stack, pc);
 }
-template <typename R, bool FLAT = false>
+template <typename R, bool FLAT = false, class STKP>
 __device__ __forceinline__ void wbvh4_round(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
-                                            int32_t* stack, unsigned long long* pc) {
-    wbvh_round_impl<R, true, FLAT>(ts, sc, ray, stack, pc);
+                                            STKP stack, unsigned long long* pc) {
+    wbvh_round_impl<R, 4, FLAT>(ts, sc, ray, stack, pc);
 }
 
 // Root and round of the tree the scene carries (4-wide when its stack bound fits).
@@ -1165,26 +1259,27 @@ template <typename R>
 __device__ __forceinline__ int32_t wbvh_root(const DSceneView<R>& sc) {
     return sc.wbvh4 ? sc.wbvh4_root : sc.wbvh_root;
 }
-template <typename R, bool FLAT = false, class SIG = NoSig>
-__device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, int32_t* stack,
+template <typename R, bool FLAT = false, class SIG = NoSig, class STKP>
+__device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, STKP stack,
                                           unsigned long long* pc = nullptr) {
     if constexpr (SIG::bvh != 0) {  // a scene-specialised kernel (jit.hip)
-        if constexpr (FLAT && NRT_WBVH_IFIF) wbvh_trip_impl<R, SIG::bvh == 4, FLAT, SIG::tie>(ts, sc, ray, stack, pc);
-        else wbvh_round_impl<R, SIG::bvh == 4, FLAT>(ts, sc, ray, stack, pc);
+        if constexpr (FLAT && NRT_WBVH_IFIF)
+            wbvh_trip_impl<R, SIG::bvh, FLAT, SIG::tie, SIG::prims>(ts, sc, ray, stack, pc);
+        else wbvh_round_impl<R, SIG::bvh, FLAT>(ts, sc, ray, stack, pc);
         return;
     }
     if constexpr (FLAT && NRT_WBVH_IFIF) {
-        if (sc.wbvh4) wbvh_trip<R, true, FLAT>(ts, sc, ray, stack, pc);
-        else wbvh_trip<R, false, FLAT>(ts, sc, ray, stack, pc);
+        if (sc.wbvh4) wbvh_trip<R, 4, FLAT>(ts, sc, ray, stack, pc);
+        else wbvh_trip<R, 2, FLAT>(ts, sc, ray, stack, pc);
     } else {
         if (sc.wbvh4) wbvh4_round<R, FLAT>(ts, sc, ray, stack, pc);
         else wbvh_round<R, FLAT>(ts, sc, ray, stack, pc);
     }
 }
 
-template <typename R, int MAXD, bool FLAT = false, class SIG = NoSig>
+template <typename R, int MAXD, bool FLAT = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ bool trace_world_bvh(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm,
-                                                int32_t* stack) {
+                                                STKP stack) {
     static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), ray);
@@ -1308,6 +1403,28 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
     return found;
 }
 
+// Stackless culling walk of the exact world mode (DThreadNode: the binary tree threaded per ray
+// octant, nearer child first): `leaf(ref)` for every reached leaf, which may lower `cut`, the
+// distance beyond which boxes are skipped.  The octant comes from the signs of the clamped 1/d,
+// the same ones that pick each box's near planes.
+template <typename R, class LEAF>
+__device__ __forceinline__ void xthread_walk(const DSceneView<R>& sc, const Ray<float>& fr, float& cut, LEAF&& leaf) {
+    const float ix = wbvh_inv(fr.d.x), iy = wbvh_inv(fr.d.y), iz = wbvh_inv(fr.d.z);
+    const float ox = fr.o.x * ix, oy = fr.o.y * iy, oz = fr.o.z * iz;
+    const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+    const int32_t n = (int32_t)sc.n_xthread;
+    const DThreadNode* base = sc.xthread + (size_t)oct * (size_t)n;
+    int32_t i = 0;
+    while (i < n) {
+        const DThreadNode nd = load16(base + i);
+        const float tn = fmaxf(fmaxf(fmaxf(nd.nearp[0] * ix - ox, nd.nearp[1] * iy - oy), nd.nearp[2] * iz - oz), 0.0f);
+        const float tf = fminf(fminf(fminf(nd.farp[0] * ix - ox, nd.farp[1] * iy - oy), nd.farp[2] * iz - oz), cut);
+        const bool hit = tn <= tf;
+        if (hit && nd.leaf != 0) leaf(nd.leaf);
+        i = (hit && nd.leaf == 0) ? i + 1 : nd.skip;
+    }
+}
+
 // Exact kernel, world-BVH mode (RenderParams::exact_wbvh; large scenes whose instances do
 // not nest, e.g. the teapot): the f32 world BVH (binned SAH, 4-wide) only culls, and every
 // primitive in a reached leaf gets the reference's own test in f64 in its object space
@@ -1317,34 +1434,30 @@ __device__ __forceinline__ bool trace_bvh(const DSceneView<R>& sc, const Ray<R>&
 // outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
 // inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
 // private array (PrivStack; the LDS holds the ChaCha8 ring and the staged scene).
-template <typename R, int MAXD, int W = 0>  // W: tree width fixed at compile time (ExactSig), 0: sc.wbvh4
-__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+// W: the culling walk fixed at compile time (ExactSig): XTHREAD_W the threaded tree, 4 / 2 the
+// stack walk of the 4-wide / binary tree; 0: chosen at run time (threaded when `thread`).
+constexpr int XTHREAD_W = 1;
+template <typename R, int MAXD, int W = 0>
+__device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
+                                                 bool thread = false) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
     fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
-    WbvhTrav ts;
-    wbvh_begin(ts, wbvh_root(sc), fr);
-    PrivStack stk;
     R best_t = R(INFINITY);
     uint32_t best_rank = 0;
     int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
     Ray<R> oray = wray;
-    while (true) {
-        while (ts.node >= 0) {
-            if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
-            else wbvh2_visit<R>(ts, sc, stk);
-        }
-        if (ts.node == WBVH_DONE) break;
-        const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
+    auto leaf_tests = [&](int32_t ref, float& cut) {
+        const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
         for (uint32_t k = 0; k < cnt; ++k) {
-            const DExactRef ref = sc.wexact[first + k];
-            if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
+            const DExactRef rf = sc.wexact[first + k];
+            if (rf.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
                 oray = wray;
-                if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
-                cur_inst = ref.inst;
+                if (rf.inst >= 0) xform_in<R, true, false>(sc, sc.instances[rf.inst], oray);
+                cur_inst = rf.inst;
             }
-            const DPrim<R>& pr = sc.prims[ref.prim];
+            const DPrim<R>& pr = sc.prims[rf.prim];
             R t;
             if (pr.kind == PRIM_SPHERE) {
                 t = sphere_t(pr, oray);
@@ -1353,14 +1466,34 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
                 V<R> point;
                 t = plane_t(pr, oray, alpha, beta, point);
             }
-            if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
+            if (t >= R(0) && (t < best_t || (t == best_t && rf.rank > best_rank))) {
                 best_t = t;
-                best_rank = ref.rank;
-                best_prim = (int32_t)ref.prim;
-                best_inst = ref.inst;
-                ts.t_best = (float)best_t * (1.0f + 0x1p-20f);
+                best_rank = rf.rank;
+                best_prim = (int32_t)rf.prim;
+                best_inst = rf.inst;
+                cut = (float)best_t * (1.0f + 0x1p-20f);
             }
         }
+    };
+    if (W == XTHREAD_W || (W == 0 && thread)) {
+        float cut = INFINITY;
+        xthread_walk(sc, fr, cut, [&](int32_t ref) { leaf_tests(ref, cut); });
+        hm.t = best_t;
+        hm.prim = (uint32_t)best_prim;
+        hm.depth = best_inst >= 0 ? 1 : 0;
+        hm.inst[0] = (uint32_t)best_inst;
+        return best_prim >= 0;
+    }
+    WbvhTrav ts;
+    wbvh_begin(ts, wbvh_root(sc), fr);
+    PrivStack stk;
+    while (true) {
+        while (ts.node >= 0) {
+            if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
+            else wbvh2_visit<R>(ts, sc, stk);
+        }
+        if (ts.node == WBVH_DONE) break;
+        leaf_tests(ts.node, ts.t_best);
         ts.node = wbvh_pop(ts, stk);
     }
     hm.t = best_t;
@@ -1503,16 +1636,25 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
 
 // The prefilter over the world-BVH walk (RenderParams::exact_pf).
 template <typename R, int MAXD, int W = 0>
-__device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+__device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
+                                                    bool thread = false) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
     fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
-    WbvhTrav ts;
-    wbvh_begin(ts, wbvh_root(sc), fr);
     XCands c;
     c.init();
-    {
+    auto offer_leaf = [&](int32_t ref, float& cut) {
+        const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
+        for (uint32_t k = 0; k < cnt; ++k)
+            if (c.offer(load16(sc.wxprims + first + k), fr, first + k)) cut = c.bound * (1.0f + 0x1p-20f);
+    };
+    if (W == XTHREAD_W || (W == 0 && thread)) {
+        float cut = INFINITY;
+        xthread_walk(sc, fr, cut, [&](int32_t ref) { offer_leaf(ref, cut); });
+    } else {
+        WbvhTrav ts;
+        wbvh_begin(ts, wbvh_root(sc), fr);
         PrivStack stk;
         while (true) {
             while (ts.node >= 0) {
@@ -1520,29 +1662,29 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
                 else wbvh2_visit<R>(ts, sc, stk);
             }
             if (ts.node == WBVH_DONE) break;
-            const uint32_t v = ~(uint32_t)ts.node, first = v >> 3, cnt = (v & 7u) + 1u;
-            for (uint32_t k = 0; k < cnt; ++k)
-                if (c.offer(load16(sc.wxprims + first + k), fr, first + k)) ts.t_best = c.bound * (1.0f + 0x1p-20f);
+            offer_leaf(ts.node, ts.t_best);
             ts.node = wbvh_pop(ts, stk);
         }
     }
-    if (c.over) return trace_exact_wbvh<R, MAXD, W>(sc, wray, hm);
+    if (c.over) return trace_exact_wbvh<R, MAXD, W>(sc, wray, hm, thread);
     return xcands_finish(c, sc, wray, hm);
 }
 
-template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                      int32_t* stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0) {
+                                      STKP stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0,
+                                      bool xthread = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
         static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
         return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);
     } else if constexpr (EXACT && sizeof(R) == 8) {
+        const bool thread = sc.xthread != nullptr && xthread;
         if constexpr (PF) {  // plane-only scenes (KF_PLANES)
-            if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm);
+            if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm, thread);
         }
-        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm);
+        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm, thread);
         return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
     } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
@@ -1569,6 +1711,9 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     if (!FLAT && kind == PRIM_SPHERE) {
         const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
         geo = normalize(h.p - center);
+        // f32-tested spheres: the hit point back on the surface (its f32 t carries a few ulp, which
+        // would leave the next ray's origin off the surface by more than the t_min of 0.001 hides)
+        if (sizeof(R) == 4 && q.AB[6] == R(0)) h.p = center + fabs(q.D) * geo;
         shade = geo;
         const R theta = acos(-geo.y);
         const R phi = atan2(-geo.z, geo.x) + R(M_PI);
@@ -1676,8 +1821,8 @@ __device__ __forceinline__ double perlin_grad(uint32_t h, double x, double y, do
     const double a = (0xCF00u & bit) ? y : x, b = (0x300Fu & bit) ? y : z;
     return ((0xEAAAu & bit) ? -a : a) + ((0x8CCCu & bit) ? -b : b);
 }
-__device__ __forceinline__ double perlin3(const float* perm, double x, double y, double z) {
-    auto P = [&](uint32_t i) { return (uint32_t)perm[i]; };
+__device__ __forceinline__ double perlin3(const uint32_t* perm, double x, double y, double z) {
+    auto P = [&](uint32_t i) { return perm[i]; };
     const double fx = floor(x), fy = floor(y), fz = floor(z);
     const uint32_t ix = (uint32_t)(long long)fx & 255u, iy = (uint32_t)(long long)fy & 255u,
                    iz = (uint32_t)(long long)fz & 255u;
@@ -1715,8 +1860,8 @@ __device__ __forceinline__ double powi_rt(double a, uint32_t b) {  // f64::powi,
 }
 // Abs<Fbm<Perlin>>::get (noise.rs:136-144, marble.rs:87-96), then the Noise / Marble
 // colour (compiled into the KF_PERLIN kernel variants only).
-__device__ __forceinline__ double perlin_texture(const float* texels, const DTexture& t, double x, double y, double z) {
-    const float* perm = texels + 3ull * t.offset;
+__device__ __forceinline__ double perlin_texture(const uint32_t* texels, const DTexture& t, double x, double y, double z) {
+    const uint32_t* perm = texels + t.offset;
     const double pz = z;
     x = x * t.color[0];
     y = y * t.color[0];
@@ -1732,6 +1877,17 @@ __device__ __forceinline__ double perlin_texture(const float* texels, const DTex
     }
     const double n = fabs(result * t.scale);
     return t.kind == TEX_NOISE ? n : (1.0 + sin(t.color[0] * pz + 10.0 * n)) / 2.0;
+}
+
+// k / 255.0f, correctly rounded, for a byte k (into_rgb32f, textures/image.rs:24-28): the product
+// with the rounded reciprocal and one Markstein correction step, exact for all 256 values (the
+// product alone is 1 ulp off for 158 of them); explicit FMAs, so the exact kernel's
+// -ffp-contract=off build computes the same
+__device__ __forceinline__ float unorm8(uint32_t k) {
+    constexpr float r = 1.0f / 255.0f;
+    const float b = (float)k;
+    const float q = b * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, b), r, q);
 }
 
 // Texture::get_color (solid_color.rs:35-43, textures/image.rs:31-40, checker.rs:76-89,
@@ -1759,8 +1915,16 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
             // reference (Q12): clamped to the last texel here.
             uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
             uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)t.b ? t.b - 1 : (uint32_t)fy);
-            const float* px = sc.texels + 3ull * (t.offset + (uint64_t)y * t.a + x);
-            return mk((R)px[0], (R)px[1], (R)px[2]);
+            if (t.format == TEXFMT_RGBA8) {  // one word (8 x 4 tiles): the three bytes, k / 255.0f exactly
+#ifdef NRT_TEX_ROWMAJOR
+                const uint32_t w = sc.texels[t.offset + (uint64_t)y * t.a + x];
+#else
+                const uint32_t w = sc.texels[t.offset + tex_tiled_index(x, y, (t.a + 7u) >> 3)];
+#endif
+                return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
+            }
+            const uint32_t* px = sc.texels + t.offset + 3ull * ((uint64_t)y * t.a + x);
+            return mk((R)__uint_as_float(px[0]), (R)__uint_as_float(px[1]), (R)__uint_as_float(px[2]));
         }
         // Checker: (uv * scale).as_u64vec2() summed, parity selects even/odd
         const R su = u * (R)t.scale, sv = v * (R)t.scale;
@@ -1854,6 +2018,9 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 
 // Philox sample pool: LDS slots per wave (a power of two; see the Philox branch of
 // render_kernel) and the pool's LDS bytes per workgroup for P pixels per group.
+#ifndef NRT_GRAB
+#define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
+#endif
 #ifndef NRT_SLOTS_LIST
 #define NRT_SLOTS_LIST 2
 #endif
@@ -1909,6 +2076,9 @@ struct MatV {
     V<R> color;
 };
 
+template <bool COMPACT> struct StackEntry { using type = int32_t; };
+template <> struct StackEntry<true> { using type = uint16_t; };
+
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0, class SIG = NoSig>
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>(KFLAGS)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
@@ -1941,9 +2111,10 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
-    // world-BVH stack (f32 kernels): the tree's bound + 1 entries
-    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(int32_t) : 0u;
-    int32_t* stack = stack_bytes ? (int32_t*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
+    // world-BVH stack (f32 kernels): the tree's bound + 1 entries (16-bit refs of the compact tree)
+    using StackT = typename StackEntry<SIG::bvh == WBVH_COMPACT>::type;
+    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(StackT) : 0u;
+    StackT* stack = stack_bytes ? (StackT*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
 
@@ -2168,7 +2339,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (traced) {
                     // world list: the global tables through the scalar cache; records read LDS
                     hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0, SIG>(
-                        MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf);
+                        MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf,
+                        p.exact_thread != 0);
                     t2 = stamp();
                 }
                 fresh = !shade(traced, hit, hm);
@@ -2216,32 +2388,50 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t cs = 0, next = GS;                 // claiming from slot cs at index next
         bool ready = false;                         // slot (cs + 1) % NS holds a group not yet claimed from
         bool exhausted = false;                     // the queue is empty
-        // Per-XCD queue heads: head x hands out the x-th contiguous eighth of the groups,
-        // and a wave pulls from its own XCD's head first (then the next heads in turn), so
-        // neighbouring groups, whose 12-B pixels share cache lines, are written out by one
-        // XCD's L2 and no head is contended by more than one XCD's waves until the tail.
-        // The XCD id only places work (any wave may pull from any head): never correctness.
+        // Group distribution: per-XCD queue heads.  Head x hands out the x-th contiguous eighth
+        // of the groups, and a wave pulls from its own XCD's head first (then the next heads in
+        // turn), so the XCD's waves work on neighbouring groups at any moment (the rays of a small
+        // image region: node, texel and framebuffer lines shared in the XCD's L1s and L2), and no
+        // head is contended by more than one XCD's waves until the tail.  A device-scope atomic
+        // executes at the memory side (one ~32-B HBM write each; with one per group they were
+        // 45 % of the C5 launch's HBM writes): a wave takes NRT_GRAB consecutive groups per atomic
+        // (more per grab spreads the XCD's waves over a larger image region: guided runs of up
+        // to 25 groups cost C4 +50 %, C5 +12 %), and skips heads an agent-scope load already
+        // shows empty (a stale value only lags).  The XCD id only places work: never correctness.
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-        uint32_t qk = 0;  // heads found empty so far (wave-uniform)
+        uint32_t qk = 0;              // heads found empty so far (wave-uniform)
+        uint32_t lcur = 0, lend = 0;  // groups of the last grab not yet taken (wave-uniform)
         auto fetch = [&](uint32_t r) {              // uniform: take the next group into (free) slot r
             uint32_t gid = 0xFFFFFFFFu;
-            if (lane == 0) {
-                for (; qk < QUEUE_HEADS; ++qk) {
-                    const uint32_t x = (xcc + qk) & (QUEUE_HEADS - 1u);
-                    const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
-                    const uint32_t hi = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS);
-                    if (hi > lo) {
-                        const uint32_t t = atomicAdd(p.queue + x * QUEUE_STRIDE, 1u);
-                        if (t < hi - lo) {
+            if (NRT_GRAB > 1 && lcur < lend) {
+                gid = lcur++;
+            } else {
+                if (lane == 0) {
+                    for (; qk < QUEUE_HEADS; ++qk) {
+                        const uint32_t x = (xcc + qk) & (QUEUE_HEADS - 1u);
+                        const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
+                        const uint32_t n = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS) - lo;
+                        unsigned int* head = p.queue + x * QUEUE_STRIDE;
+                        if (n == 0 || __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n)
+                            continue;
+                        const uint32_t k = qk ? 1u : (uint32_t)NRT_GRAB;  // a steal takes one group
+                        const uint32_t t = atomicAdd(head, k);
+                        if (t < n) {
                             gid = lo + t;
+                            lcur = gid + 1u;
+                            lend = lo + min(t + k, n);
                             break;
                         }
                     }
                 }
+                gid = __builtin_amdgcn_readlane(gid, 0);
+                qk = __builtin_amdgcn_readlane(qk, 0);
+                if (NRT_GRAB > 1) {
+                    lcur = __builtin_amdgcn_readlane(lcur, 0);
+                    lend = __builtin_amdgcn_readlane(lend, 0);
+                }
             }
-            gid = __builtin_amdgcn_readlane(gid, 0);
-            qk = __builtin_amdgcn_readlane(qk, 0);
             exhausted = gid == 0xFFFFFFFFu;  // (plain stores and selects: the flags stay in registers)
             if (exhausted) return;
             const uint32_t base = p.pixel_begin + gid * P;
@@ -2363,7 +2553,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 // world list: the global tables through the scalar cache; records read LDS
                 if (traced)
                     hit = trace<R, MAXD, EXACT, FLAT, false, SIG>(MAXD == 0 ? gsc : sc, ray, hm, stack,
-                                                                   p.exact_all != 0, p.exact_wbvh != 0);
+                                                                   p.exact_all != 0, p.exact_wbvh != 0, 0u,
+                                                                   p.exact_thread != 0);
             }
             const unsigned long long t1 = stamp();
             Rec<R> h;

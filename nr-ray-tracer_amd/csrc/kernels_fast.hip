@@ -22,7 +22,7 @@ void launch_fast(const RenderParams& p, const DSceneView<float>& v, uint32_t rng
 }
 
 void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* fnp, uint32_t lds_fixed, int maxd,
-                     uint32_t rng, hipStream_t stream) {
+                     uint32_t rng, uint32_t stack_entry, hipStream_t stream) {
     const hipFunction_t fn = (hipFunction_t)fnp;
     auto resident = [&](uint32_t lds) {
         int per_cu = 0, dev_id = 0, cus = 0;
@@ -40,7 +40,7 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
         if (hipModuleLaunchKernel(fn, blocks, 1, 1, dev::BLOCK, 1, 1, lds, stream, args, nullptr) != hipSuccess)
             throw std::runtime_error("HIP error in hipModuleLaunchKernel (scene-specialised kernel)");
     };
-    const uint32_t stack = maxd == MODE_WORLD_BVH ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0u;
+    const uint32_t stack = maxd == MODE_WORLD_BVH ? (v.wbvh_stack + 1u) * dev::BLOCK * stack_entry : 0u;
     if (rng == RNG_CHACHA8) {  // one lane per pixel (launch_variant): ring + stack below the staged scene
         const uint32_t npix = p0.pixel_end - p0.pixel_begin;
         launch((npix + dev::BLOCK - 1) / dev::BLOCK, lds_fixed + dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) + stack, p0);

@@ -41,8 +41,9 @@ struct JitStats {
 void* jit_render_kernel(const std::string& targs, int device);
 JitStats jit_stats();
 uint64_t jit_compile_only(const std::string& targs, std::string* log);  // code bytes, 0 on failure (tests)
+// stack_entry: bytes per world-BVH stack entry (2 for the compact tree, kernel.hpp StackEntry)
 void launch_fast_jit(const RenderParams& p, const DSceneView<float>& v, void* fn, uint32_t lds_fixed, int maxd,
-                     uint32_t rng, hipStream_t stream);
+                     uint32_t rng, uint32_t stack_entry, hipStream_t stream);
 void launch_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample,
                       unsigned long long* d_out);
 

@@ -102,6 +102,12 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     if constexpr (sizeof(R) == 8 && MAXD == 1 && G::exact_stream) {
         if (planes && !perlin && !p.counters) {  // KF_PLANES: the 4-wave f64 variant
             if (p.exact_wbvh && p.exact_pf && !p.exact_all) {  // the prefiltered world walk only
+                if (p.exact_thread && v.xthread) {  // the stackless threaded walk
+                    using XT = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, dev::XTHREAD_W>;
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XT>(p, v, ring + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XT>(p, v, ring, stream);
+                    return;
+                }
                 // (tree width left to the run time: fixing it measured C5 -0.3 %, C4 +2.8 %)
                 using XS = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, 0>;
                 if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XS>(p, v, ring + scene, stream);

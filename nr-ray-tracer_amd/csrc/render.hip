@@ -54,6 +54,7 @@ struct DeviceScene {
     bool flat = false;      // world list without spheres, solid colours only (KF_FLAT variants)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
+    int wbvh_kinds = 0;  // WPRIMS_* of the world BVH's leaves (the scene-specialised kernel's BvhSig)
     std::vector<uint32_t> wruns;  // the world list's run words (scene-specialised kernel, jit.hip)
     // Philox group-queue heads: each launch takes the next of QUEUE_SLOTS sets of
     // QUEUE_HEADS per-XCD heads and zeroes it on its own stream (up to QUEUE_SLOTS
@@ -110,7 +111,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* inst = (DInstance*)track(upload(fs.instances, "instances"), fs.instances.size() * sizeof(DInstance));
         auto* mats = (DMaterial*)track(upload(fs.materials, "materials"), fs.materials.size() * sizeof(DMaterial));
         auto* texs = (DTexture*)track(upload(fs.textures, "textures"), fs.textures.size() * sizeof(DTexture));
-        auto* texels = (float*)track(upload(fs.texels, "texels"), fs.texels.size() * sizeof(float));
+        auto* texels = (uint32_t*)track(upload(fs.texels, "texels"), fs.texels.size() * sizeof(uint32_t));
         auto* fpr = (DPrimFast<float>*)track(upload(f32.fprims, "fprims"), f32.fprims.size() * sizeof(DPrimFast<float>));
         auto* ifast = (DInstFast<float>*)track(upload(f32.inst_fast, "inst_fast"),
                                                f32.inst_fast.size() * sizeof(DInstFast<float>));
@@ -121,6 +122,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         auto* wrn = (uint32_t*)track(upload(wruns_padded, "wruns"), wruns_padded.size() * sizeof(uint32_t));
         auto* wbn = (DBvhNode*)track(upload(fs.wbvh.nodes, "wbvh"), fs.wbvh.nodes.size() * sizeof(DBvhNode));
         auto* wb4 = (DBvh4Node*)track(upload(fs.wbvh.nodes4, "wbvh4"), fs.wbvh.nodes4.size() * sizeof(DBvh4Node));
+        auto* wb4c = (DBvh4cNode*)track(upload(fs.wbvh.nodes4c, "wbvh4c"), fs.wbvh.nodes4c.size() * sizeof(DBvh4cNode));
         auto* wbp = (DPrimWorld<float>*)track(upload(f32.wbvh_prims, "wbvh_prims"),
                                               f32.wbvh_prims.size() * sizeof(DPrimWorld<float>));
         const uint32_t np = (uint32_t)fs.prims.size(), nx = (uint32_t)fs.xforms.size(),
@@ -143,12 +145,14 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
             xb4 = (DBvh4Node*)track(upload(xt.nodes4, "wbvh4_x"), xt.nodes4.size() * sizeof(DBvh4Node));
         }
         const bool x4 = !xt.nodes4.empty() && use_wbvh4(fs);
+        auto* xth = (DThreadNode*)track(upload(xt.threaded, "wbvh_threaded"), xt.threaded.size() * sizeof(DThreadNode));
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
                                      nullptr, 0, nullptr, 0, 0, wx_ok ? xbn : nullptr,
-                                     (wx_ok && x4) ? xb4 : nullptr, xt.root4, xt.root,
+                                     (wx_ok && x4) ? xb4 : nullptr, nullptr, xt.root4, xt.root,
                                      wx_ok ? (uint32_t)xt.nodes.size() : 0u,
-                                     std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? wx : nullptr,
+                                     std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? xth : nullptr,
+                                     wx_ok ? xt.threaded_n : 0u, wx_ok ? wx : nullptr,
                                      wx_ok ? wxp : nullptr, wx_ok ? (uint32_t)fs.wexact.size() : 0u};
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
@@ -156,8 +160,8 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)f32.fprims.size(), (uint32_t)f32.inst_fast.size(),
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
                                     (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
-                                    fs.wbvh.root4, fs.wbvh.root,
-                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, nullptr, 0u};
+                                    use_wbvh4(fs) ? wb4c : nullptr, fs.wbvh.root4, fs.wbvh.root,
+                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, 0u, nullptr, nullptr, 0u};
         ds->wbvh_ok = fs.wbvh_ok;
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->planes = !fs.prims.empty();
@@ -173,6 +177,16 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         track(ds->queues, qbytes);
         check(hipMemset(ds->queues, 0, qbytes), "hipMemset(queues)");
         ds->n_wbvh_prims = (uint32_t)f32.wbvh_prims.size();
+        {
+            bool tri = false, quad = false, other = false;
+            for (const DPrimWorld<float>& w : f32.wbvh_prims) {
+                const uint32_t k = w.meta & WKIND_MASK;
+                tri |= k == PRIM_TRIANGLE;
+                quad |= k == PRIM_QUAD;
+                other |= k != PRIM_TRIANGLE && k != PRIM_QUAD;
+            }
+            ds->wbvh_kinds = other || (tri && quad) ? WPRIMS_ANY : (quad ? WPRIMS_QUADS : WPRIMS_TRIANGLES);
+        }
         ds->world_ok = fs.world_ok;
         ds->list_ok = fs.list_ok;
         ds->world_units = fs.world_units;
@@ -251,6 +265,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         // scene-specialised kernel (jit.hip): the world list's run words, or the world BVH's
         // width and tie flag, as template arguments; the same LDS layout as launch_one
         void* jit = nullptr;
+        uint32_t stack_entry = 4;  // bytes per world-BVH stack entry of the kernel launched
         const uint32_t scene_lds = lds_scene_bytes(v);
         const bool staged = scene_lds <= LDS_SCENE_LIMIT;
         const uint32_t lds_fixed = staged ? scene_lds : 0u;  // (+ the BVH stack: launch_fast_jit)
@@ -268,12 +283,16 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
                     jit = jit_render_kernel(targs + ">", ds->device);
                 }
             } else if (ds->flat) {  // (if-if trips: teapot 41.1 -> 40.5 ms; the sphere rounds measured slower)
-                targs += std::string("nrt::dev::BvhSig<") + (v.wbvh4 ? "4, " : "2, ") +
-                         ((v.wflags & WFLAG_COPLANAR) ? "true>" : "false>");
+                // the compact 4-wide tree where the scene has one (knob NRT_WBVH_COMPACT=0: the 64-byte one)
+                const char* ce = std::getenv("NRT_WBVH_COMPACT");
+                const bool compact = v.wbvh4c && !(ce && ce[0] == '0');
+                if (compact) stack_entry = 2;
+                targs += std::string("nrt::dev::BvhSig<") + (compact ? "5, " : v.wbvh4 ? "4, " : "2, ") +
+                         ((v.wflags & WFLAG_COPLANAR) ? "true, " : "false, ") + std::to_string(ds->wbvh_kinds) + ">";
                 jit = jit_render_kernel(targs, ds->device);
             }
         }
-        if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, rng, stream);
+        if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, rng, jit ? stack_entry : 4u, stream);
         else launch_fast(q, v, rng, maxd, ds->perlin, ds->flat, stream);
     }
     check(hipGetLastError(), "render kernel launch");

@@ -44,6 +44,7 @@ struct Builder {
     std::vector<Item> items;
     WorldBvh out;
     double pad = 0.0;
+    uint32_t leaf_max = WBVH_LEAF_MAX;
 
     static constexpr int BINS = 16;
 
@@ -128,10 +129,10 @@ struct Builder {
         const double split_cost = 1.0 + best_cost / std::max(all.area(), 1e-300);
         size_t mid;
         if (best_axis < 0) {  // all centroids coincide: split by count
-            if (n <= WBVH_LEAF_MAX) return leaf(b, e);
+            if (n <= leaf_max) return leaf(b, e);
             mid = b + n / 2;
         } else {
-            if (n <= WBVH_LEAF_MAX && leaf_cost <= split_cost) return leaf(b, e);
+            if (n <= leaf_max && leaf_cost <= split_cost) return leaf(b, e);
             const double ext = cb.hi[best_axis] - cb.lo[best_axis], scale = BINS / ext;
             auto it = std::partition(items.begin() + b, items.begin() + e, [&](const Item& x) {
                 int k = (int)((x.c[best_axis] - cb.lo[best_axis]) * scale);
@@ -232,8 +233,88 @@ struct Collapse {
 
 }  // namespace
 
-WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const std::vector<float>& cost) {
+// The compact form of nodes4 (device_scene.hpp DBvh4cNode), or empty when a ref does not fit.
+static std::vector<DBvh4cNode> compact_nodes(const std::vector<DBvh4Node>& n4, size_t slots) {
+    std::vector<DBvh4cNode> out;
+    if (n4.size() >= WBVH4C_MAX_NODES || slots >= WBVH4C_MAX_PRIMS) return out;
+    out.resize(n4.size());
+    for (size_t i = 0; i < n4.size(); ++i) {
+        const DBvh4Node& a = n4[i];
+        DBvh4cNode& c = out[i];
+        std::memset(&c, 0, sizeof c);
+        for (int k = 0; k < 3; ++k) {
+            c.org[k] = a.org[k];
+            c.qlo[k] = a.qlo[k];
+            c.qhi[k] = a.qhi[k];
+        }
+        c.exps = a.exps;
+        for (int k = 0; k < 4; ++k) {
+            const int32_t r = a.child[k];
+            if (r == WBVH_DONE) {
+                c.child[k] = 0;  // empty slot: its box is never hit
+            } else if (r >= 0) {
+                c.child[k] = (uint16_t)r;
+            } else {
+                const uint32_t v = ~(uint32_t)r, first = v >> 3, cnt = (v & 7u) + 1u;
+                if (cnt > WBVH4C_LEAF_MAX) return {};
+                c.child[k] = (uint16_t)(WBVH4C_LEAF | first << 2 | (cnt - 1u));
+            }
+        }
+    }
+    return out;
+}
+
+// The binary tree threaded in depth-first order for octant `oct` (device_scene.hpp DThreadNode):
+// nearer child first along the octant's diagonal, planes as (near, far).
+static void thread_tree(const std::vector<DBvhNode>& nodes, int32_t root, int oct, std::vector<DThreadNode>& out) {
+    const float sg[3] = {(oct & 1) ? -1.0f : 1.0f, (oct & 2) ? -1.0f : 1.0f, (oct & 4) ? -1.0f : 1.0f};
+    const size_t base = out.size();
+    auto emit = [&](auto&& self, int32_t ref, const float* lo, const float* hi) -> void {
+        const size_t idx = out.size();
+        DThreadNode t{};
+        for (int k = 0; k < 3; ++k) {
+            t.nearp[k] = sg[k] > 0 ? lo[k] : hi[k];
+            t.farp[k] = sg[k] > 0 ? hi[k] : lo[k];
+        }
+        t.leaf = ref < 0 ? ref : 0;
+        out.push_back(t);
+        if (ref >= 0) {
+            const DBvhNode& b = nodes[(size_t)ref];
+            float d0 = 0, d1 = 0;
+            for (int k = 0; k < 3; ++k) {
+                d0 += sg[k] * (b.lo0[k] + b.hi0[k]);
+                d1 += sg[k] * (b.lo1[k] + b.hi1[k]);
+            }
+            if (d0 <= d1) {
+                self(self, b.c0, b.lo0, b.hi0);
+                self(self, b.c1, b.lo1, b.hi1);
+            } else {
+                self(self, b.c1, b.lo1, b.hi1);
+                self(self, b.c0, b.lo0, b.hi0);
+            }
+        }
+        out[idx].skip = (int32_t)(out.size() - base);
+    };
+    // the root's box: the union of its children's, or everything for a single leaf
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = -3e38f;
+        hi[k] = 3e38f;
+    }
+    if (root >= 0) {
+        const DBvhNode& b = nodes[(size_t)root];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(b.lo0[k], b.lo1[k]);
+            hi[k] = std::max(b.hi0[k], b.hi1[k]);
+        }
+    }
+    if (root != WBVH_DONE) emit(emit, root, lo, hi);
+}
+
+WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const std::vector<float>& cost,
+                         uint32_t leaf_max) {
     Builder bld;
+    bld.leaf_max = std::max<uint32_t>(1u, std::min(leaf_max, WBVH_LEAF_MAX));
     bld.items.resize(bounds.size());
     double scale = 0.0;
     for (size_t i = 0; i < bounds.size(); ++i) {
@@ -249,6 +330,7 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
         it.cost = i < cost.size() ? cost[i] : 1.0f;
     }
     bld.pad = 1e-6 * std::max(scale, 1e-30);  // flat (axis-plane) primitives keep a volume
+    bld.out.scale = scale;
     if (!bounds.empty()) bld.out.root = bld.build(0, bld.items.size(), 0);
     if (bld.out.depth > WBVH_STACK) throw std::runtime_error("world BVH deeper than the kernel's stack");
     if (bld.out.root >= 0) {
@@ -271,9 +353,12 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
             bld.out.nodes4.clear();
             bld.out.root4 = WBVH_DONE;
         }
+        bld.out.nodes4c = compact_nodes(bld.out.nodes4, bld.out.order.size());
     } else {
         bld.out.root4 = bld.out.root;  // a single leaf (or empty)
     }
+    for (int oct = 0; oct < 8; ++oct) thread_tree(bld.out.nodes, bld.out.root, oct, bld.out.threaded);
+    bld.out.threaded_n = (uint32_t)(bld.out.threaded.size() / 8);
     return std::move(bld.out);
 }
 

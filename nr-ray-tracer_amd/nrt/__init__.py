@@ -70,7 +70,7 @@ class _SceneStats(C.Structure):
                 ("materials", C.c_uint64), ("textures", C.c_uint64), ("texels", C.c_uint64), ("trees", C.c_uint32),
                 ("max_instance_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("world_prims", C.c_uint64),
                 ("coplanar_pairs", C.c_uint32), ("world_list_ok", C.c_uint32), ("exact_mode", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("texel_bytes", C.c_uint32)]
 
 
 PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)

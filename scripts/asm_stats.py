@@ -1,6 +1,6 @@
 """Static instruction mix and register use of one render-kernel variant (device-only compile, no GPU).
 
-usage: python scripts/asm_stats.py [mangled-name fragment] [-DFLAG ...]
+usage: python scripts/asm_stats.py [--exact] [mangled-name fragment] [-DFLAG ...]
        python scripts/asm_stats.py --targs "float, nrt::dev::Philox, -1, false, false, 4, nrt::dev::BvhSig<4, false>"
 default fragment: the headline kernel (f32, Philox, world list, LDS scene, KF_FLAT) of kernels_fast.hip.
 --targs: the template arguments of a scene-specialised kernel (jit.hip builds them with hiprtc; the
@@ -25,6 +25,11 @@ def main():
     pkg = os.path.join(ROOT, "nr-ray-tracer_amd")
     inc = ["-I" + os.path.join(pkg, "csrc"), "-I" + os.path.join(ROOT, "include")]
     td = tempfile.mkdtemp()
+    flags = list(FLAGS)
+    if args and args[0] == "--exact":  # the exact kernels' contraction (kernels_exact.hip: none)
+        flags = [f if f != "-ffp-contract=fast" else "-ffp-contract=off" for f in flags]
+        flags = [f for f in flags if f not in ("-mllvm", "-amdgpu-use-amdgpu-trackers")]
+        args = args[1:]
     if args and args[0] == "--targs":
         targs = args[1]
         args = args[2:]
@@ -38,7 +43,7 @@ def main():
         frag = args.pop(0) if args and not args[0].startswith("-") else "PhiloxELi0ELb0ELb1ELi4EE"
         src = os.path.join(pkg, "csrc", "kernels_fast.hip")
     out = os.path.join(td, "all.s")
-    r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *inc, src, "-o", out, *args], cwd=pkg, capture_output=True,
+    r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, *inc, src, "-o", out, *args], cwd=pkg, capture_output=True,
                        text=True)
     if r.returncode != 0:
         sys.exit(r.stderr[-3000:])

@@ -32,7 +32,10 @@ def main():
                 out["avg_ns"] = float(r["AverageNs"])
     agg = collections.defaultdict(float)
     disp = collections.defaultdict(set)
-    for f in glob.glob(os.path.join(a.dir, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+    files = glob.glob(os.path.join(a.dir, "pmc*", "**", "*counter_collection.csv"), recursive=True)
+    if not files:  # a single PMC pass's output directory
+        files = glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)
+    for f in files:
         for r in csv.DictReader(open(f)):
             if a.kernel in r.get("Kernel_Name", ""):
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])

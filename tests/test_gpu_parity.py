@@ -308,3 +308,23 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     assert np.isfinite(base).all()
     for name, img in frames.items():
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
+
+
+def test_exact_world_mode_far_camera(monkeypatch):
+    """The exact world mode culls with f32 boxes padded by 1e-6 of the scene's extent, enough for
+    ray origins within ~7x that extent; a camera farther out makes make_params (api.cpp) take the
+    reference tree or the all-primitives walk, even when the knobs force the world walk, so the
+    frame stays the reference's (camera.rs:244-267 rays from look_from, object.rs:89-121)."""
+    w, h, spp = 24, 16, 2
+    with in_golden():
+        s = nrt.Scene.load("scenes/cornell-box-scene.json",
+                           nrt.CameraConfig(width=w, height=h, samples_per_pixel=spp, look_from=(0.5, 0.5, -60.0),
+                                            field_of_view=2.0))
+    frames = []
+    for env in (("0", "0", "0"), ("0", "1", "1")):  # reference tree; forced world walk + prefilter
+        monkeypatch.setenv("NRT_EXACT_ALL", env[0])
+        monkeypatch.setenv("NRT_EXACT_WBVH", env[1])
+        monkeypatch.setenv("NRT_EXACT_PF", env[2])
+        frames.append(s.render(precision="f64", rng="chacha8"))
+    assert np.isfinite(frames[0]).all() and frames[0].max() > 0
+    np.testing.assert_array_equal(frames[1].view(np.uint32), frames[0].view(np.uint32))
