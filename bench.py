@@ -327,13 +327,22 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in kev) / max(len(kev), 1)
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
     jit_after = nrt.jit_stats()
+    specialised = jit_after["launches"] - jit_before["launches"] >= args.steps
+    mixed = False
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        # max over ranks of the times; min and max over ranks of "timed on the scene-specialised kernel"
+        # (its f32 frames may differ in the last bits from the generic kernel's: a mix would make the
+        # assembled frame depend on which rank's hiprtc build failed)
+        t = torch.tensor([elapsed, kern_ms, float(specialised), -float(specialised)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+        mixed = float(t[2]) != -float(t[3])
 
-    kernel_variant = "scene-specialised (hiprtc)" if jit_after["launches"] - jit_before["launches"] >= args.steps \
-        else "generic"
+    kernel_variant = "scene-specialised (hiprtc)" if specialised else "generic"
+    if mixed:
+        kernel_variant = "MIXED over ranks (scene-specialised on some, generic on others)"
+        print("bench.py: WARNING: ranks ran different kernel variants", file=sys.stderr, flush=True)
     if jit_after["failed"]:
         kernel_variant = "generic (scene-specialised build FAILED)"
         print(f"bench.py: WARNING: {jit_after['failed']} scene-specialised kernel build(s) failed; the generic "

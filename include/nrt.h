@@ -170,6 +170,13 @@ int nrt_camera_config_apply(const nrt_camera_config* cfg, nrt_camera_builder* b)
  *      the file (nested scenes, textures) resolve against the process CWD, as in
  *      the reference.  `overrides` may be NULL. */
 int nrt_scene_load(const char* path, const nrt_camera_config* overrides, nrt_scene** out, nrt_camera* camera);
+/* The same with load flags: NRT_LOAD_LEGACY_SCHEMA also accepts the legacy index schema of
+ * scenes/triangles.toml (integer texture / material references, `objects`), mapped onto the
+ * current one with ids "0", "1", ... (what `create triangles` writes today, create/triangles.rs).
+ * Without it the file fails to load (NRT_E_LOAD), as in the reference. */
+enum { NRT_LOAD_LEGACY_SCHEMA = 1u << 0 };
+int nrt_scene_load_ex(const char* path, const nrt_camera_config* overrides, uint32_t flags, nrt_scene** out,
+                      nrt_camera* camera);
 
 /* ---- scene from the library constructors (the Hitable/Material/Texture
  *      trait surface of nr-ray-tracer-lib).  Handles are small non-negative

@@ -240,7 +240,9 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // plane-only scenes: the exact world mode's f32 prefilter (knob NRT_EXACT_PF=0 turns it off;
     // over every slot instead of the walk measured slower on Cornell, 223 against 217 ms)
     p.exact_pf = 1;
-    p.exact_thread = 1;  // knob NRT_EXACT_THREAD=0: the 4-wide stack walk (round 2)
+    // the stackless threaded walk of the culling tree (no private stack; knob NRT_EXACT_THREAD=1) measured
+    // slower than the 4-wide walk with its private stack: C5 f64 spp 64 69.2 vs 57.7 ms, C4 128.3 vs 98.6
+    p.exact_thread = 0;
     if (const char* e = std::getenv("NRT_EXACT_THREAD")) p.exact_thread = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;
@@ -387,12 +389,18 @@ int nrt_camera_config_apply(const nrt_camera_config* cfg, nrt_camera_builder* b)
 }
 
 int nrt_scene_load(const char* path, const nrt_camera_config* overrides, nrt_scene** out, nrt_camera* camera) {
+    return nrt_scene_load_ex(path, overrides, 0u, out, camera);
+}
+
+int nrt_scene_load_ex(const char* path, const nrt_camera_config* overrides, uint32_t flags, nrt_scene** out,
+                      nrt_camera* camera) {
     if (out) *out = nullptr;
     return guarded(NRT_E_LOAD, [&]() {
         if (!path || !out) throw std::invalid_argument("null argument");
+        if (flags & ~(uint32_t)NRT_LOAD_LEGACY_SCHEMA) throw std::invalid_argument("unknown load flags");
         CameraConfig cli;
         if (overrides) cli = from_c(*overrides);
-        LoadedScene ls = load_scene_file(path, overrides ? &cli : nullptr);
+        LoadedScene ls = load_scene_file(path, overrides ? &cli : nullptr, (flags & NRT_LOAD_LEGACY_SCHEMA) != 0);
         auto s = std::make_unique<nrt_scene>();
         s->graph = ls.objects;
         s->flat = flatten_scene(ls.objects);

@@ -2,7 +2,8 @@
 // command (packages/ray-tracer/src/commands/render.rs:104-115, cli.rs:111-270):
 // same flags and NR_RT_CAMERA_* environment variables, render timed alone
 // (render.rs:57-62), gamma 0.5 + to_rgb8 + write (render.rs:74-102).
-// Extra flags: --precision {f64,f32}, --rng {chacha8,philox}, --gpus N.
+// Extra flags: --precision {f64,f32}, --rng {chacha8,philox}, --gpus N, --legacy-schema (also
+// load the index schema of scenes/triangles.toml, NRT_LOAD_LEGACY_SCHEMA).
 // Output formats: .png (stored deflate), .ppm, .pfm (linear f32).
 //
 // `nrt-cli convert-stl <STL> [-o FILE] [-f] [-F toml|json]` — the reference's
@@ -216,7 +217,7 @@ void usage() {
             "       [--background-color X,Y,Z] [--look-at X,Y,Z] [--look-from X,Y,Z] [--view-up X,Y,Z]\n"
             "       [--focal-length F] [--field-of-view DEG] [--defocus-angle DEG] [--focus-distance D]\n"
             "       [--samples-per-pixel N] [--ray-max-bounces N] [-v]\n"
-            "       [--precision f64|f32] [--rng chacha8|philox] [--gpus N]\n");
+            "       [--precision f64|f32] [--rng chacha8|philox] [--gpus N] [--legacy-schema]\n");
     exit(2);
 }
 
@@ -227,6 +228,7 @@ int main(int argc, char** argv) {
     if (argc < 3 || std::string(argv[1]) != "render") usage();
     std::string scene, output = "out.png";
     bool force = false, verbose = false;
+    uint32_t load_flags = 0;
     float gamma = 0.5f;
     int gpus = 1;
     nrt_camera_config cc{};
@@ -309,7 +311,7 @@ int main(int argc, char** argv) {
 
     nrt_scene* sc = nullptr;
     nrt_camera cam{};
-    if (nrt_scene_load(scene.c_str(), &cc, &sc, &cam) != NRT_OK) die(nrt_last_error());
+    if (nrt_scene_load_ex(scene.c_str(), &cc, load_flags, &sc, &cam) != NRT_OK) die(nrt_last_error());
     const uint32_t W = (uint32_t)cam.width, H = (uint32_t)cam.height;
     std::vector<float> img((size_t)W * H * 3);
 

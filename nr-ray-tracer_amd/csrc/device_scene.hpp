@@ -346,6 +346,12 @@ struct DSceneView {
     uint32_t n_wexact;                 // slots of that tree
 };
 
+// World primitives staged in LDS sit 80 bytes apart (64-byte records + 16 bytes of padding): the
+// lanes of a ds_read_b128 group that read different records then start on different banks of
+// the 64 (a 64-byte stride puts every fourth record on the same banks: the hit-record reads
+// made 46 % of the headline kernel's LDS cycles conflict cycles).
+constexpr uint32_t WPRIM_LDS_STRIDE = 80;
+
 // Bytes of the LDS-stageable part of a scene (everything but texels), each
 // array starting on a 16-byte boundary, in the order nodes, prims, xforms,
 // instances, materials, textures.
@@ -356,7 +362,7 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
            r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>)) +
-           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * sizeof(DPrimWorld<Real>));
+           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * WPRIM_LDS_STRIDE);
 }
 
 }  // namespace nrt

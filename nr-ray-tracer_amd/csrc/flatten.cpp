@@ -818,11 +818,12 @@ struct Flattener {
                 }
                 // AB[6] = 1: tested in f64 (spheres larger than the scene scale)
                 const double sl = std::sqrt(w.AB[0] * w.AB[0] + w.AB[1] * w.AB[1] + w.AB[2] * w.AB[2]);
-                static const bool f32_ok = [] {  // knob NRT_SPHERE_F32=0: every sphere in f64 (A/B runs)
+                // knob NRT_SPHERE_F32 (A/B runs): 0 every sphere in f64, 2 every sphere in f32
+                static const int f32_mode = [] {
                     const char* e = std::getenv("NRT_SPHERE_F32");
-                    return !(e && e[0] == '0');
+                    return e ? (int)std::strtol(e, nullptr, 10) : 1;
                 }();
-                w.AB[6] = f32_ok && cl + sl + ar <= SPHERE_F32_EXTENT ? 0.0 : 1.0;
+                w.AB[6] = f32_mode == 2 || (f32_mode == 1 && cl + sl + ar <= SPHERE_F32_EXTENT) ? 0.0 : 1.0;
                 const uint32_t mat = material(o->material);
                 if (mat > WMAT_MASK) { out.world_ok = false; return; }
                 w.meta = PRIM_SPHERE | (mat << WKIND_BITS);

@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
                 for (float v : img.rgb) sum += v;
                 if (!quiet) std::printf("ok   %s %ux%u sum %.6f\n", path.c_str(), img.width, img.height, sum);
             } else {
-                const LoadedScene sc = load_scene_file(path, nullptr);
+                const LoadedScene sc = load_scene_file(path, nullptr, ends_with(path, "triangles.toml"));
                 const FlatScene flat = flatten_scene(sc.objects);
                 const FlatScene32 f32 = to_f32(flat);
                 const std::string dump = dump_graph(sc.objects);

@@ -43,6 +43,9 @@ constexpr int BLOCK = 256;
 // Msamples/s); scenes with f64 sphere tests keep the speculative rounds (C1 -27 % if-if)
 #define NRT_WBVH_IFIF 1
 #endif
+#ifndef NRT_SPHERE_REPROJ
+#define NRT_SPHERE_REPROJ 1  // f32-tested spheres: hit points put back on the surface (make_record_world)
+#endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 
 template <typename R>
@@ -1693,11 +1696,12 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
 // World-space record (MAXD <= 0; device_scene.hpp DPrimWorld): the
 // reference's front-face sign signum(d'.n) = signum(d.(M^T n)), shading normal
 // mapped out by the chain's rotations only.
-template <typename R, int MAXD, bool FLAT = false>
+template <typename R, int MAXD, bool FLAT = false, bool STAGED = false>  // STAGED: sc.wprims in LDS (80-B stride)
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
     // hm.prim is always a primitive record: box and room hits name their face quad
-    const DPrimWorld<R> q = load16(sc.wprims + hm.prim);
+    const DPrimWorld<R> q = load16(STAGED ? (const DPrimWorld<R>*)((const unsigned char*)sc.wprims + hm.prim * WPRIM_LDS_STRIDE)
+                                          : sc.wprims + hm.prim);
     R t = hm.t;  // world BVH: the closest key = t scaled by the winner's coplanar-tie factor (WCLASS_*)
     if (MAXD < 0 && (sc.wflags & WFLAG_COPLANAR)) {
         const uint32_t cls = q.meta >> WCLASS_SHIFT;
@@ -1713,7 +1717,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
         geo = normalize(h.p - center);
         // f32-tested spheres: the hit point back on the surface (its f32 t carries a few ulp, which
         // would leave the next ray's origin off the surface by more than the t_min of 0.001 hides)
-        if (sizeof(R) == 4 && q.AB[6] == R(0)) h.p = center + fabs(q.D) * geo;
+        if (NRT_SPHERE_REPROJ && sizeof(R) == 4 && q.AB[6] == R(0)) h.p = center + fabs(q.D) * geo;
         shade = geo;
         const R theta = acos(-geo.y);
         const R phi = atan2(-geo.z, geo.x) + R(M_PI);
@@ -1805,9 +1809,9 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     return h;
 }
 
-template <typename R, int MAXD, bool EXACT, bool FLAT = false>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool STAGED = false>
 __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
-    if constexpr (MAXD <= 0) return make_record_world<R, MAXD, FLAT>(sc, wray, hm);
+    if constexpr (MAXD <= 0) return make_record_world<R, MAXD, FLAT, STAGED>(sc, wray, hm);
     else return make_record_bvh<R, MAXD, EXACT>(sc, wray, hm);
 }
 
@@ -1975,7 +1979,14 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.fprims = (const DPrimFast<R>*)copy(g.fprims, g.n_fprims * (uint32_t)sizeof(DPrimFast<R>));
     s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
     s.mats_fast = (const DMatFast*)copy(g.mats_fast, g.n_mats_fast * (uint32_t)sizeof(DMatFast));
-    s.wprims = (const DPrimWorld<R>*)copy(g.wprims, g.n_wprims * (uint32_t)sizeof(DPrimWorld<R>));
+    {  // world primitives WPRIM_LDS_STRIDE bytes apart (device_scene.hpp)
+        unsigned char* dst = base + off;
+        const uint4* s4 = (const uint4*)g.wprims;
+        constexpr uint32_t Q = (uint32_t)sizeof(DPrimWorld<R>) / 16u, QS = WPRIM_LDS_STRIDE / 16u;
+        for (uint32_t k = threadIdx.x; k < g.n_wprims * Q; k += BLOCK) ((uint4*)dst)[(k / Q) * QS + k % Q] = s4[k];
+        off += (g.n_wprims * WPRIM_LDS_STRIDE + 15u) & ~15u;
+        s.wprims = (const DPrimWorld<R>*)dst;
+    }
     __syncthreads();
     return s;
 }
@@ -2171,7 +2182,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             contrib = tp * cam(6);  // background
             return false;
         }
-        h = make_record<R, MAXD, EXACT, FLAT>(sc, ray, hm);
+        h = make_record<R, MAXD, EXACT, FLAT, LDS_SCENE>(sc, ray, hm);
         m = material(h.mat);
         if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:62-75), no scatter
             const R k = bounced ? m.param : R(1.0);

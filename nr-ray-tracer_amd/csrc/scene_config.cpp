@@ -220,7 +220,9 @@ MaterialPtr get_material(const Value* id, const MaterialMap& materials, const Ma
 // and `materials` are arrays of variant tables referenced by integer index and the
 // objects sit in `objects`.  It maps onto the current schema with ids "0", "1", ...
 // -- the scene `nr-ray-tracer create triangles` now writes with named ids
-// (create/triangles.rs:10-86).  Other documents are returned unchanged.
+// (create/triangles.rs:10-86).  Other documents are returned unchanged.  Opt-in
+// (NRT_LOAD_LEGACY_SCHEMA): the reference's SceneConfig rejects the file (serde expects
+// (id, config) pairs) and ignores an unknown `objects` key of a current-schema document.
 Value legacy_refs(const Value& v) {
     Value out = v;
     if (v.kind == Value::Table) {
@@ -267,6 +269,7 @@ Value normalize_legacy(const Value& doc) {
 
 struct Builder {
     int depth = 0;
+    bool legacy = false;  // accept the legacy index schema of scenes/triangles.toml (opt-in)
 
     // SceneConfig::try_build_aux (scene_config.rs:410-473)
     LoadedScene build_aux(const Value& doc, const MaterialPtr* material_fallback_in, const CameraConfig* cli) {
@@ -347,7 +350,7 @@ struct Builder {
             MaterialPtr m = get_material(opt(b, "material"), materials, fallback);
             const std::string path = as_str(req(b, "path", "Scene"), "path");
             if (++depth > 64) fail("nested Scene depth exceeds 64 (recursive scene file?)");
-            LoadedScene child = build_aux(load_doc(path), &m, nullptr);
+            LoadedScene child = build_aux(load_doc(path, legacy), &m, nullptr);
             --depth;
             return child.objects;
         }
@@ -371,14 +374,17 @@ struct Builder {
         fail("unknown variant `" + kind + "` for ObjectConfig");
     }
 
-    // SceneConfig::try_load_scene (scene_config.rs:475-492): format by extension
-    static Value load_doc(const std::string& path) {
+    // SceneConfig::try_load_scene (scene_config.rs:475-492): format by extension; the legacy
+    // schema is mapped onto the current one only on request (the reference itself rejects it)
+    static Value load_doc(const std::string& path, bool legacy) {
         const size_t dot = path.find_last_of('.');
         const size_t slash = path.find_last_of('/');
         const std::string ext = (dot == std::string::npos || (slash != std::string::npos && dot < slash)) ? "" : path.substr(dot + 1);
-        if (ext == "json") return normalize_legacy(parse_json(read_file(path)));
-        if (ext == "toml") return normalize_legacy(parse_toml(read_file(path)));
-        fail("invalid scene file format!");
+        Value doc;
+        if (ext == "json") doc = parse_json(read_file(path));
+        else if (ext == "toml") doc = parse_toml(read_file(path));
+        else fail("invalid scene file format!");
+        return legacy ? normalize_legacy(doc) : doc;
     }
 };
 
@@ -434,9 +440,10 @@ void CameraConfig::try_update(CameraBuilder& b) const {
     if (has_look_from) b.look_from = look_from;
 }
 
-LoadedScene load_scene_file(const std::string& path, const CameraConfig* cli) {
+LoadedScene load_scene_file(const std::string& path, const CameraConfig* cli, bool legacy_schema) {
     Builder b;
-    Value doc = Builder::load_doc(path);
+    b.legacy = legacy_schema;
+    Value doc = Builder::load_doc(path, legacy_schema);
     return b.build_aux(doc, nullptr, cli);
 }
 

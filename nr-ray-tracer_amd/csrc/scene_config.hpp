@@ -31,8 +31,9 @@ struct LoadedScene {
     Camera camera;
 };
 
-// SceneConfig::try_load_scene + merge_with(cli) + try_build  (render.rs:107-111)
-LoadedScene load_scene_file(const std::string& path, const CameraConfig* cli_overrides);
+// SceneConfig::try_load_scene + merge_with(cli) + try_build  (render.rs:107-111); legacy_schema:
+// also accept the index schema of scenes/triangles.toml (normalize_legacy)
+LoadedScene load_scene_file(const std::string& path, const CameraConfig* cli_overrides, bool legacy_schema = false);
 
 // Decoded Rgb32F image (u8/255 per channel), ImageReader::decode().into_rgb32f().
 struct DecodedImage {

@@ -88,6 +88,8 @@ SIGNATURES = {
     "nrt_camera_build": (C.c_int, [C.POINTER(_CameraBuilder), C.POINTER(_Camera)]),
     "nrt_camera_config_apply": (C.c_int, [C.POINTER(_CameraConfig), C.POINTER(_CameraBuilder)]),
     "nrt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_CameraConfig), C.POINTER(C.c_void_p), C.POINTER(_Camera)]),
+    "nrt_scene_load_ex": (C.c_int, [C.c_char_p, C.POINTER(_CameraConfig), C.c_uint32, C.POINTER(C.c_void_p),
+                                    C.POINTER(_Camera)]),
     "nrt_builder_new": (C.c_void_p, []),
     "nrt_builder_free": (None, [C.c_void_p]),
     "nrt_texture_solid": (C.c_int32, [C.c_void_p, _D3]),
@@ -350,11 +352,13 @@ class Scene:
         self.camera = camera
 
     @staticmethod
-    def load(path: str, overrides: Optional[CameraConfig] = None) -> "Scene":
+    def load(path: str, overrides: Optional[CameraConfig] = None, legacy_schema: bool = False) -> "Scene":
+        """SceneConfig::try_load_scene + merge_with + try_build; legacy_schema also accepts the index
+        schema of scenes/triangles.toml (nrt_scene_load_ex, NRT_LOAD_LEGACY_SCHEMA)."""
         h = C.c_void_p()
         cam = _Camera()
         ov = C.byref(overrides._c()) if overrides is not None else None
-        _check(lib().nrt_scene_load(os.fsencode(path), ov, C.byref(h), C.byref(cam)))
+        _check(lib().nrt_scene_load_ex(os.fsencode(path), ov, 1 if legacy_schema else 0, C.byref(h), C.byref(cam)))
         return Scene(h.value, Camera._from_c(cam))
 
     def close(self) -> None:

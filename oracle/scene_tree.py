@@ -224,9 +224,10 @@ class TreeWriter:
 
 
 class Builder:
-    def __init__(self, w: TreeWriter):
+    def __init__(self, w: TreeWriter, legacy: bool = False):
         self.w = w
         self.depth = 0
+        self.legacy = legacy
 
     def make_texture(self, cfg: Any, textures: dict) -> int:  # scene_config.rs:52-123
         kind, b = _variant(cfg, "texture config")
@@ -317,7 +318,7 @@ class Builder:
             self.depth += 1
             if self.depth > 64:
                 raise LoadError("nested scene too deep")
-            root, _ = self.build_aux(load_doc(b["path"]), m, None)
+            root, _ = self.build_aux(load_doc(b["path"], self.legacy), m, None)
             self.depth -= 1
             return root
         if kind == "Ref":
@@ -401,7 +402,7 @@ def normalize_legacy(doc: Any) -> Any:
     return out
 
 
-def load_doc(path: str) -> Any:  # scene_config.rs:475-492
+def load_doc(path: str, legacy: bool = False) -> Any:  # scene_config.rs:475-492
     ext = os.path.splitext(path)[1]
     if ext not in (".json", ".toml"):
         raise LoadError("invalid scene file format!")
@@ -409,15 +410,16 @@ def load_doc(path: str) -> Any:  # scene_config.rs:475-492
         raise LoadError(f"No such file or directory (os error 2): {path}")
     with open(path, "rb") as fh:
         raw = fh.read()
-    if ext == ".json":
-        return normalize_legacy(json.loads(raw.decode("utf-8")))
-    return normalize_legacy(tomli.loads(raw.decode("utf-8")))
+    doc = json.loads(raw.decode("utf-8")) if ext == ".json" else tomli.loads(raw.decode("utf-8"))
+    return normalize_legacy(doc) if legacy else doc  # the legacy schema only on request
 
 
-def build_tree(path: str, overrides: CameraConfig | None, texel_dir: str) -> tuple[str, CameraBuilder]:
-    """SceneConfig::try_load_scene + merge_with(cli) + try_build -> tree text."""
+def build_tree(path: str, overrides: CameraConfig | None, texel_dir: str,
+               legacy: bool = False) -> tuple[str, CameraBuilder]:
+    """SceneConfig::try_load_scene + merge_with(cli) + try_build -> tree text (legacy: also the
+    index schema of scenes/triangles.toml, mapped by normalize_legacy)."""
     w = TreeWriter(texel_dir)
-    root, cam = Builder(w).build_aux(load_doc(path), None, overrides)
+    root, cam = Builder(w, legacy).build_aux(load_doc(path, legacy), None, overrides)
     head = ("CAMERA {} {} {} {} ".format(cam.width, cam.height, cam.samples_per_pixel, cam.ray_max_bounces)
             + " ".join(_f(x) for x in (*cam.background_color, *cam.look_from, *cam.look_at, *cam.view_up))
             + f" {_f(cam.defocus_angle)} {_f(cam.focus_dist)} {_f(cam.field_of_view)}")

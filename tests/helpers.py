@@ -30,13 +30,18 @@ def ensure_oracle():
     return ORACLE_BIN
 
 
+def is_legacy(scene):
+    """Scene files in the legacy index schema (loaded with the explicit opt-in)."""
+    return scene.endswith("triangles.toml")
+
+
 def oracle_tree(scene, workdir, width=None, height=None, spp=None, bounces=None):
     """Independent Python loader -> oracle tree file (path)."""
     from oracle import scene_tree
 
     cli = scene_tree.CameraConfig(width=width, height=height, samples_per_pixel=spp, ray_max_bounces=bounces)
     with in_golden():
-        text, cam = scene_tree.build_tree(scene, cli, workdir)
+        text, cam = scene_tree.build_tree(scene, cli, workdir, legacy=is_legacy(scene))
     path = os.path.join(workdir, os.path.basename(scene) + ".tree")
     with open(path, "w") as fh:
         fh.write(text)

@@ -14,7 +14,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from helpers import GOLDEN, in_golden, oracle_render, oracle_tree
+from helpers import is_legacy, GOLDEN, in_golden, oracle_render, oracle_tree
 
 IMAGES = os.path.join(GOLDEN, "images")
 with open(os.path.join(IMAGES, "manifest.json")) as _fh:
@@ -57,7 +57,8 @@ def test_exact_kernel_matches_fixture(name):
     with in_golden():
         s = nrt.Scene.load(c["scene"], nrt.CameraConfig(width=c["width"], height=c["height"],
                                                         samples_per_pixel=c["spp"],
-                                                        ray_max_bounces=c["ray_max_bounces"]))
+                                                        ray_max_bounces=c["ray_max_bounces"]),
+                           legacy_schema=is_legacy(c["scene"]))
     got = s.render(precision="f64", rng="chacha8").reshape(-1)
     assert np.all(np.isfinite(got))
     same = np.mean(got == want)

@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 import nrt
-from helpers import in_golden, oracle_render, oracle_tree
+from helpers import in_golden, is_legacy, oracle_render, oracle_tree
 
 pytestmark = pytest.mark.gpu
 
@@ -43,7 +43,7 @@ CASES_F64 = [
 def load(scene, w, h, spp, bounces=None):
     with in_golden():
         return nrt.Scene.load(scene, nrt.CameraConfig(width=w, height=h, samples_per_pixel=spp,
-                                                      ray_max_bounces=bounces))
+                                                      ray_max_bounces=bounces), legacy_schema=is_legacy(scene))
 
 
 def reference(scene, w, h, spp, bounces=None, rows=(0, 1)):

@@ -11,7 +11,7 @@ import tempfile
 import pytest
 
 import nrt
-from helpers import in_golden, oracle_dump, oracle_tree
+from helpers import in_golden, is_legacy, oracle_dump, oracle_tree
 
 # (scene, overrides) — every scene file in the reference that its own loader accepts
 LOADABLE = [
@@ -36,7 +36,7 @@ def product_dump(scene, ov):
     cfg = nrt.CameraConfig(width=ov.get("width"), height=ov.get("height"), samples_per_pixel=ov.get("spp"),
                            ray_max_bounces=ov.get("bounces"))
     with in_golden():
-        s = nrt.Scene.load(scene, cfg)
+        s = nrt.Scene.load(scene, cfg, legacy_schema=is_legacy(scene))
     c = s.camera
 
     def hx3(v):
@@ -139,6 +139,7 @@ def test_legacy_triangles_equal_current_schema(tmp_path):
 @pytest.mark.parametrize("scene,code", [
     ("scenes/does-not-exist.json", -2),
     ("scenes/textures/earth.jpg", -2),       # not a scene format
+    ("scenes/triangles.toml", -2),           # legacy index schema: rejected by default, as by the reference
 ])
 def test_load_errors(scene, code):
     with in_golden():
@@ -161,3 +162,23 @@ def test_size_rules():
         s = nrt.Scene.load("scenes/cornell-box-scene.json")
         assert (s.camera.width, s.camera.height) == (1200, 800)  # CameraBuilder default
         assert s.camera.samples_per_pixel == 200 and s.camera.ray_max_bounces == 50
+
+
+def test_legacy_schema_is_opt_in(tmp_path):
+    """The reference's SceneConfig (scene_config.rs:384-404) expects (id, config) pairs and ignores
+    an unknown `objects` key: scenes/triangles.toml fails to load and a current-schema document with
+    `objects` but no `scene` loads as an empty scene, unless the legacy schema is asked for
+    (nrt_scene_load_ex NRT_LOAD_LEGACY_SCHEMA); the oracle's loader agrees on both."""
+    from oracle import scene_tree
+
+    with in_golden():
+        with pytest.raises(scene_tree.LoadError):
+            scene_tree.load_doc("scenes/triangles.toml") and scene_tree.build_tree(
+                "scenes/triangles.toml", None, str(tmp_path))
+        s = nrt.Scene.load("scenes/triangles.toml", nrt.CameraConfig(width=8, height=8), legacy_schema=True)
+        assert s.stats()["prims"] > 0
+    doc = tmp_path / "objects-only.json"
+    doc.write_text('{"camera": {}, "objects": [{"Sphere": {"center": [0, 0, 0], "radius": 1.0}}]}')
+    empty = nrt.Scene.load(str(doc), nrt.CameraConfig(width=8, height=8))
+    assert empty.stats()["prims"] == 0
+    assert nrt.Scene.load(str(doc), nrt.CameraConfig(width=8, height=8), legacy_schema=True).stats()["prims"] == 1
