@@ -244,6 +244,8 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // slower than the 4-wide walk with its private stack: C5 f64 spp 64 69.2 vs 57.7 ms, C4 128.3 vs 98.6
     p.exact_thread = 0;
     if (const char* e = std::getenv("NRT_EXACT_THREAD")) p.exact_thread = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+    p.exact_lstack = 0;  // knob NRT_EXACT_LSTACK=1: the compact walk's stack in LDS at 3 waves per SIMD
+    if (const char* e = std::getenv("NRT_EXACT_LSTACK")) p.exact_lstack = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
@@ -253,14 +255,6 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // knob NRT_WAVE_PIXELS (a power of two 1..128).  ChaCha8 streams are sequential:
     // one lane per pixel.
     p.wave_pixels = 1;
-    // Philox group distribution: 90 % of each eighth's groups statically, round-robin over the
-    // waves of its label, the rest through the per-label queue head (one device-scope atomic per
-    // group: those run at the memory side, ~32 B of HBM writes each); knob NRT_STATIC_SHARE 0..1024
-    p.static_share = 922;
-    if (const char* e = std::getenv("NRT_STATIC_SHARE")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 0 && v <= 1024) p.static_share = (uint32_t)v;
-    }
     if (o && o->rng == NRT_RNG_PHILOX) {
         p.wave_pixels = 0;
         if (const char* e = std::getenv("NRT_WAVE_PIXELS")) {

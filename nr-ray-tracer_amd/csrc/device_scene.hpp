@@ -126,6 +126,10 @@ constexpr double SPHERE_F32_EXTENT = 100.0;
 // world y slab of axis quads and rooms (t = fma(Y, 1/d_y, -o_y/d_y)); face slots as
 // PRIM_BOX with axis 1 = y (side 0 = bottom).
 constexpr uint32_t PRIM_BOXY = 8;
+// PRIM_SPHERE32 (world-list run kind only; the unit's meta kind stays PRIM_SPHERE): spheres the
+// f32 test takes (AB[6] = 0).  A PRIM_SPHERE run is tested in f64 only, so a scene-specialised
+// kernel compiles one sphere test per unit instead of both (C3 earth: 2350 -> 2063 instructions).
+constexpr uint32_t PRIM_SPHERE32 = 9;
 // PRIM_ABOX (world list): axis quads that each cover a whole face of one axis-
 // aligned box (a "room": the Cornell walls) as one slab test; header N = lo,
 // AB[0..2] = hi, meta = PRIM_ABOX | face slots << 3 (3 bits per (axis, side),
@@ -350,19 +354,22 @@ struct DSceneView {
 // lanes of a ds_read_b128 group that read different records then start on different banks of
 // the 64 (a 64-byte stride puts every fourth record on the same banks: the hit-record reads
 // made 46 % of the headline kernel's LDS cycles conflict cycles).
+// World-list mode only (MAXD 0): the world-BVH modes read staged records for the hit record
+// alone, and the padding would cost them LDS occupancy (spheres.toml: 490 records).
 constexpr uint32_t WPRIM_LDS_STRIDE = 80;
+constexpr uint32_t wprim_lds_stride(int maxd) { return maxd == 0 ? WPRIM_LDS_STRIDE : 64u; }
 
 // Bytes of the LDS-stageable part of a scene (everything but texels), each
 // array starting on a 16-byte boundary, in the order nodes, prims, xforms,
 // instances, materials, textures.
 template <typename Real>
-inline uint32_t lds_scene_bytes(const DSceneView<Real>& v) {
+inline uint32_t lds_scene_bytes(const DSceneView<Real>& v, int maxd) {
     auto r16 = [](uint64_t b) { return (uint32_t)((b + 15) & ~uint64_t(15)); };
     return r16(v.n_nodes * sizeof(DNode<Real>)) + r16(v.n_prims * sizeof(DPrim<Real>)) +
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
            r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>)) +
-           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * WPRIM_LDS_STRIDE);
+           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * wprim_lds_stride(maxd));
 }
 
 }  // namespace nrt

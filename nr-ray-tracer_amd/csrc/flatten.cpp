@@ -59,6 +59,11 @@ struct Flattener {
                     const float k = std::nearbyint(v * 255.0f);
                     unorm8 = k >= 0.0f && k <= 255.0f && (float)k / 255.0f == v && !std::signbit(v);
                 }
+                static const bool rgba8_ok = [] {  // knob NRT_TEX_RGBA8=0 (A/B runs): keep RGB32F texels
+                    const char* e = std::getenv("NRT_TEX_RGBA8");
+                    return !(e && e[0] == '0');
+                }();
+                unorm8 &= rgba8_ok;
                 d.format = unorm8 ? TEXFMT_RGBA8 : TEXFMT_RGB32F;
                 if (unorm8) {  // 8 x 4 texel tiles of one 128-byte line each, rows of tiles (tex_texel_index)
                     const uint32_t tw = (t->width + 7u) / 8u, th = (t->height + 3u) / 4u;
@@ -1089,8 +1094,14 @@ struct Flattener {
         out.wprims.swap(fused);
         out.world_units = kinds.size();
         const uint32_t one = 1u << WRUN_KIND_BITS;
-        for (uint32_t kind : kinds) {
-            if (kind >= PRIM_QUAD_X) out.wflags |= WFLAG_AXIS_QUADS;  // axis quads, rooms and y boxes use 1/d
+        size_t at = 0;  // first entry of the unit
+        for (size_t u = 0; u < kinds.size(); ++u) {
+            uint32_t kind = kinds[u];
+            const size_t first = at;
+            at += units[order[u]].size();
+            if (kind == PRIM_SPHERE && out.wprims[first].AB[6] == 0.0) kind = PRIM_SPHERE32;
+            if (kind >= PRIM_QUAD_X && kind != PRIM_SPHERE32)
+                out.wflags |= WFLAG_AXIS_QUADS;  // axis quads, rooms and y boxes use 1/d
             if (!out.wruns.empty() && (out.wruns.back() & WRUN_KIND_MASK) == kind &&
                 (out.wruns.back() >> WRUN_KIND_BITS) < (1u << 27))
                 out.wruns.back() += one;

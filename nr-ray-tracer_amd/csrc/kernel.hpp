@@ -37,6 +37,9 @@ constexpr int BLOCK = 256;
 #ifndef NRT_WBVH_SORT
 #define NRT_WBVH_SORT 0  // 4-wide visits: 1 = full sorting network; 0 = nearest hit child first, the rest in slot order (C4 +4 %)
 #endif
+#ifndef NRT_LEAF_PER_TRIP
+#define NRT_LEAF_PER_TRIP 1  // if-if trips: primitives of a leaf one lane tests per trip
+#endif
 #ifndef NRT_WBVH_IFIF
 // world BVH: one node visit or one primitive per lane and trip (wbvh_trip) in the KF_FLAT
 // variant (triangles / quads only: a primitive costs a fifth of a visit; C4 6 307 -> 6 400
@@ -561,14 +564,14 @@ __device__ __forceinline__ float sphere_t_world_f32(const Q& q, const Ray<float>
     const float t = tn > 0.001f ? tn : tf;
     return ((disc >= 0.0f) & (t > 0.001f) & (t < INFINITY)) ? t : -1.0f;
 }
-// The world modes' sphere test: f32 (above) for spheres within the scene's scale (AB[6] = 0:
-// |center| + |speed| + |r| <= SPHERE_F32_EXTENT, flatten.cpp), whose hit points the record then
-// puts back on the surface (make_record_world); the quadratic in f64 for the large ones (the
-// r = 1e5 and r = 1e3 ground spheres): their f32 hit points would sit up to ~1e-5 off a surface
-// of that size, and the next ray's t_min = 0.001 would not hide the self-intersection.
+// The world modes' sphere tests: f32 (above) for the world list's PRIM_SPHERE32 runs, spheres
+// within the scene's scale (AB[6] = 0: |center| + |speed| + |r| <= SPHERE_F32_EXTENT, flatten.cpp),
+// whose hit points the record then puts back on the surface (make_record_world); the quadratic in
+// f64 (below) for the large ones (the r = 1e5 and r = 1e3 ground spheres: their f32 hit points would
+// sit up to ~1e-5 off a surface of that size, and the next ray's t_min = 0.001 would not hide the
+// self-intersection), and for every sphere of a world-BVH leaf (world_prim_t).
 template <class Q>
-__device__ __forceinline__ float sphere_t_world(const Q& q, const Ray<float>& r) {
-    if (q.AB[6] == 0.0f) return sphere_t_world_f32(q, r);
+__device__ __forceinline__ float sphere_t_world_f64(const Q& q, const Ray<float>& r) {
     DPrim<float> sp;
     for (int c = 0; c < 3; ++c) { sp.a[c] = q.N[c]; sp.b[c] = q.AB[c]; }
     sp.s = q.D;
@@ -797,9 +800,18 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
         }
         return;
     }
-    if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres (not compiled in)
+    if (!FLAT && kind == PRIM_SPHERE32) {  // FLAT: the scene has no spheres (not compiled in)
         for (; k < end; ++k) {
-            const float t = sphere_t_world(wp[k], ray);
+            const float t = sphere_t_world_f32(wp[k], ray);
+            const bool ok = (t >= 0.0f) & (t <= t_best);
+            t_best = ok ? t : t_best;
+            best = ok ? (int32_t)k : best;
+        }
+        return;
+    }
+    if (!FLAT && kind == PRIM_SPHERE) {  // the large spheres, in f64
+        for (; k < end; ++k) {
+            const float t = sphere_t_world_f64(wp[k], ray);
             const bool ok = (t >= 0.0f) & (t <= t_best);
             t_best = ok ? t : t_best;
             best = ok ? (int32_t)k : best;
@@ -833,6 +845,7 @@ struct NoSig {
     static constexpr bool tie = false;
     static constexpr int prims = 0;  // world-BVH leaf primitive kinds (WPRIMS_*), 0: decided per primitive
     static constexpr int exact = 0;  // exact kernel: traversal fixed at compile time (ExactSig), 0: runtime
+    static constexpr bool lstack = false;
 };
 template <uint32_t... RUNS>
 struct WorldSig {
@@ -841,19 +854,21 @@ struct WorldSig {
     static constexpr bool tie = false;
     static constexpr int prims = 0;
     static constexpr int exact = 0;
+    static constexpr bool lstack = false;
 };
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
 // the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
 // plane-only scenes, and the unfiltered walk it falls back to).
 enum : int { EXACT_SIG_WORLD_PF = 1 };
-template <int MODE, int WIDTH>
+template <int MODE, int WIDTH, bool LSTACK = false>
 struct ExactSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = WIDTH;  // culling walk: 4 / 2 the stack walk of that width, XTHREAD_W the
-                                       // threaded tree, 0: chosen at run time
+                                       // threaded tree, WBVH_COMPACT the compact tree, 0: chosen at run time
     static constexpr bool tie = false;
     static constexpr int prims = 0;
     static constexpr int exact = MODE;
+    static constexpr bool lstack = LSTACK;  // compact walk: its 16-bit stack in LDS (fewer waves), not scratch
 };
 // World-BVH mode (jit.hip): the tree's width (2 or 4), whether it holds coplanar-tie keys
 // (WFLAG_COPLANAR) and which primitive kinds its leaves hold (WPRIMS_*) as constants, so one
@@ -865,6 +880,7 @@ struct BvhSig {
     static constexpr bool tie = TIE;
     static constexpr int prims = PRIMS;
     static constexpr int exact = 0;
+    static constexpr bool lstack = false;
 };
 template <bool FLAT, uint32_t... RUNS>
 __device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float> wp, uint32_t& k, const Ray<float>& ray,
@@ -924,7 +940,9 @@ template <bool FLAT = false, bool TIE = false, int PRIMS = 0>  // PRIMS: WPRIMS_
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
     const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
     if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres
-        const float t = sphere_t_world(q, ray);
+        // in f64: the f32 test of small spheres beside it took the generic world-BVH kernel to
+        // 129 VGPRs, 3 waves per SIMD (spheres.toml 1080p 34.9 -> 39.9 ms)
+        const float t = sphere_t_world_f64(q, ray);
         return (t >= 0.0f && t <= t_best) ? t : -1.0f;
     }
     const V<float> nrm = ld3(q.N);
@@ -1025,6 +1043,11 @@ __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc,
 struct PrivStack {
     int32_t e[WBVH_STACK + 1];
 };
+// the compact tree's raw 16-bit refs (exact kernel, ExactSig width WBVH_COMPACT): half the
+// scratch bytes per push
+struct PrivStack16 {
+    uint16_t e[WBVH_STACK + 1];
+};
 __device__ __forceinline__ void stk_write(int32_t* s, uint32_t k, int32_t v) { s[k * BLOCK] = v; }
 __device__ __forceinline__ int32_t stk_read(int32_t* s, uint32_t k) { return s[k * BLOCK]; }
 // compact 4-wide tree (BvhSig width WBVH_COMPACT): the raw 16-bit child refs
@@ -1032,6 +1055,8 @@ __device__ __forceinline__ void stk_write(uint16_t* s, uint32_t k, int32_t v) { 
 __device__ __forceinline__ int32_t stk_read(uint16_t* s, uint32_t k) { return (int32_t)s[k * BLOCK]; }
 __device__ __forceinline__ void stk_write(PrivStack& s, uint32_t k, int32_t v) { s.e[k] = v; }
 __device__ __forceinline__ int32_t stk_read(PrivStack& s, uint32_t k) { return s.e[k]; }
+__device__ __forceinline__ void stk_write(PrivStack16& s, uint32_t k, int32_t v) { s.e[k] = (uint16_t)v; }
+__device__ __forceinline__ int32_t stk_read(PrivStack16& s, uint32_t k) { return (int32_t)s.e[k]; }
 template <class STK>
 __device__ __forceinline__ int32_t wbvh_pop(WbvhTrav& ts, STK& stack) {
     return ts.sp ? stk_read(stack, --ts.sp) : WBVH_DONE;
@@ -1122,6 +1147,12 @@ __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc
     t.node = t0 != INFINITY ? c0 : wbvh_pop(t, stack);
 }
 
+#ifndef NRT_PK_SLAB
+#define NRT_PK_SLAB 0  // (near, far) pairs as v_pk_fma_f32: C4 40.2 -> 41.1 ms, off
+#endif
+#ifndef NRT_NODE_MIX
+#define NRT_NODE_MIX 0
+#endif
 // Compact 4-wide visit (DBvh4cNode: the same boxes, 16-bit child refs; three loads instead of
 // four).  The stack holds the raw 16-bit refs; a ref becomes the traversal's 32-bit form
 // (inner index, or ~(first << 3 | count - 1) for a leaf) only when it is taken (wbvh4c_ref).
@@ -1134,6 +1165,7 @@ __device__ __forceinline__ int32_t wbvh4c_pop(WbvhTrav& ts, STK& stack) {
 }
 template <typename R, class STK>
 __device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
+    // (an LDS copy of the tree's top levels, breadth-first numbered, measured C4 40.2 -> 43.8 ms)
     const DBvh4cNode nd = load16(sc.wbvh4c + t.node);
     const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
     const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
@@ -1142,16 +1174,67 @@ __device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& s
     const uint32_t nqx = px ? nd.qlo[0] : nd.qhi[0], fqx = px ? nd.qhi[0] : nd.qlo[0];
     const uint32_t nqy = py ? nd.qlo[1] : nd.qhi[1], fqy = py ? nd.qhi[1] : nd.qlo[1];
     const uint32_t nqz = pz ? nd.qlo[2] : nd.qhi[2], fqz = pz ? nd.qhi[2] : nd.qlo[2];
+#if NRT_NODE_MIX
+    // Plane bytes without byte -> float conversions (quarter-rate v_cvt_f32_ubyte*): one v_perm_b32
+    // turns two bytes q of a word into the f16 pair 1024 + q (0x64 high bytes), and v_fma_mix_f32
+    // reads either half as an f16 operand: (1024 + q) * A + (B - 1024 A).  The folded offset
+    // rounds B - 1024 A to f32, an error of ~2^-14 of a quantization step in t (the decode's own
+    // f32 rounding is of that order).
+    uint32_t k64, sel01, sel23;
+    asm volatile("s_mov_b32 %0, 0x64646464" : "=s"(k64));
+    asm volatile("s_mov_b32 %0, 0x04010400" : "=s"(sel01));
+    asm volatile("s_mov_b32 %0, 0x04030402" : "=s"(sel23));
+    const float Cx = __builtin_fmaf(-1024.0f, Ax, Bx), Cy = __builtin_fmaf(-1024.0f, Ay, By),
+                Cz = __builtin_fmaf(-1024.0f, Az, Bz);
+    auto pairs = [&](uint32_t w, uint32_t sel) {
+        uint32_t r;
+        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "s"(k64), "v"(w), "s"(sel));
+        return r;
+    };
+    auto mix_lo = [](uint32_t h, float a, float c) {
+        float r;
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(a), "v"(c));
+        return r;
+    };
+    auto mix_hi = [](uint32_t h, float a, float c) {
+        float r;
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(a), "v"(c));
+        return r;
+    };
+    float tc[4];
+#pragma unroll
+    for (int hp = 0; hp < 2; ++hp) {  // children (0, 1), then (2, 3)
+        const uint32_t sel = hp ? sel23 : sel01;
+        const uint32_t nx = pairs(nqx, sel), fx = pairs(fqx, sel), ny = pairs(nqy, sel), fy = pairs(fqy, sel),
+                       nz = pairs(nqz, sel), fz = pairs(fqz, sel);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            auto m = [&](uint32_t h, float a, float c) { return j ? mix_hi(h, a, c) : mix_lo(h, a, c); };
+            const float n = fmaxf(fmaxf(m(nx, Ax, Cx), m(ny, Ay, Cy)), fmaxf(m(nz, Az, Cz), 0.0f));
+            const float f = fminf(fminf(m(fx, Ax, Cx), m(fy, Ay, Cy)), fminf(m(fz, Az, Cz), t.t_best));
+            tc[2 * hp + j] = n <= f ? n : INFINITY;
+        }
+    }
+    float t0 = tc[0], t1 = tc[1], t2 = tc[2], t3 = tc[3];
+#else
     auto child_t = [&](int k) {  // entry distance of child k, +inf if missed or empty
         auto q = [&](uint32_t w) { return (float)((w >> (8 * k)) & 0xFFu); };
+#if NRT_PK_SLAB
+        const f32x2 x = f32x2{q(nqx), q(fqx)} * Ax + Bx;  // (near, far) plane pairs: v_pk_fma_f32
+        const f32x2 y = f32x2{q(nqy), q(fqy)} * Ay + By;
+        const f32x2 z = f32x2{q(nqz), q(fqz)} * Az + Bz;
+        const float nx = x.x, fx = x.y, ny = y.x, fy = y.y, nz = z.x, fz = z.y;
+#else
         const float nx = q(nqx) * Ax + Bx, fx = q(fqx) * Ax + Bx;
         const float ny = q(nqy) * Ay + By, fy = q(fqy) * Ay + By;
         const float nz = q(nqz) * Az + Bz, fz = q(fqz) * Az + Bz;
+#endif
         const float n = fmaxf(fmaxf(nx, ny), fmaxf(nz, 0.0f));
         const float f = fminf(fminf(fx, fy), fminf(fz, t.t_best));
         return n <= f ? n : INFINITY;
     };
     float t0 = child_t(0), t1 = child_t(1), t2 = child_t(2), t3 = child_t(3);
+#endif
     const uint32_t c01 = (uint32_t)nd.child[0] | ((uint32_t)nd.child[1] << 16);
     const uint32_t c23 = (uint32_t)nd.child[2] | ((uint32_t)nd.child[3] << 16);
     int32_t c0 = (int32_t)(c01 & 0xFFFFu), c1 = (int32_t)(c01 >> 16), c2 = (int32_t)(c23 & 0xFFFFu),
@@ -1170,7 +1253,7 @@ __device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& s
 // Visit / pop of a tree of width W (2 binary, 4 four-wide, WBVH_COMPACT the compact four-wide)
 template <int W, typename R, class STK>
 __device__ __forceinline__ void wbvh_visit_w(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
-    if constexpr (W == WBVH_COMPACT) wbvh4c_visit(t, sc, stack);
+    if constexpr (W == WBVH_COMPACT) wbvh4c_visit<R>(t, sc, stack);
     else if constexpr (W == 4) wbvh4_visit(t, sc, stack);
     else wbvh2_visit(t, sc, stack);
 }
@@ -1223,13 +1306,17 @@ __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>
                                                STKP stack, unsigned long long* pc) {
     if (ts.leaf != WBVH_NO_LEAF) {
         prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
-        const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
-        const DPrimWorld<float> q = load16(sc.wprims + first);
-        const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
-        const bool ok = t >= 0.0f;
-        ts.t_best = ok ? t : ts.t_best;
-        ts.best = ok ? (int32_t)first : ts.best;
-        ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+#pragma unroll
+        for (int u = 0; u < NRT_LEAF_PER_TRIP; ++u) {  // up to NRT_LEAF_PER_TRIP primitives of the leaf
+            if (u > 0 && ts.leaf == WBVH_NO_LEAF) break;
+            const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
+            const DPrimWorld<float> q = load16(sc.wprims + first);
+            const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
+            const bool ok = t >= 0.0f;
+            ts.t_best = ok ? t : ts.t_best;
+            ts.best = ok ? (int32_t)first : ts.best;
+            ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+        }
     } else if (ts.node >= 0) {
         prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
         wbvh_visit_w<W>(ts, sc, stack);
@@ -1440,9 +1527,9 @@ __device__ __forceinline__ void xthread_walk(const DSceneView<R>& sc, const Ray<
 // W: the culling walk fixed at compile time (ExactSig): XTHREAD_W the threaded tree, 4 / 2 the
 // stack walk of the 4-wide / binary tree; 0: chosen at run time (threaded when `thread`).
 constexpr int XTHREAD_W = 1;
-template <typename R, int MAXD, int W = 0>
+template <typename R, int MAXD, int W = 0, bool PLANES = false, bool LSTACK = false>  // PLANES: no spheres
 __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                                 bool thread = false) {
+                                                 bool thread = false, uint16_t* lstk = nullptr) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
@@ -1462,7 +1549,7 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
             }
             const DPrim<R>& pr = sc.prims[rf.prim];
             R t;
-            if (pr.kind == PRIM_SPHERE) {
+            if (!PLANES && pr.kind == PRIM_SPHERE) {
                 t = sphere_t(pr, oray);
             } else {
                 R alpha, beta;
@@ -1489,15 +1576,32 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
     }
     WbvhTrav ts;
     wbvh_begin(ts, wbvh_root(sc), fr);
-    PrivStack stk;
-    while (true) {
-        while (ts.node >= 0) {
-            if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
-            else wbvh2_visit<R>(ts, sc, stk);
+    if constexpr (W == WBVH_COMPACT) {
+        auto walk = [&](auto& stk) {
+            while (true) {
+                while (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
+                if (ts.node == WBVH_DONE) break;
+                leaf_tests(ts.node, ts.t_best);
+                ts.node = wbvh4c_pop(ts, stk);
+            }
+        };
+        if constexpr (LSTACK) {
+            walk(lstk);
+        } else {
+            PrivStack16 stk;
+            walk(stk);
         }
-        if (ts.node == WBVH_DONE) break;
-        leaf_tests(ts.node, ts.t_best);
-        ts.node = wbvh_pop(ts, stk);
+    } else {
+        PrivStack stk;
+        while (true) {
+            while (ts.node >= 0) {
+                if (W == 4 || (W == 0 && sc.wbvh4)) wbvh4_visit<R>(ts, sc, stk);
+                else wbvh2_visit<R>(ts, sc, stk);
+            }
+            if (ts.node == WBVH_DONE) break;
+            leaf_tests(ts.node, ts.t_best);
+            ts.node = wbvh_pop(ts, stk);
+        }
     }
     hm.t = best_t;
     hm.prim = (uint32_t)best_prim;
@@ -1602,7 +1706,9 @@ struct XCands {
     }
 };
 // Phase 2: the reference tests on the surviving candidates (smallest exact t, ties to the
-// higher depth-first rank, as trace_exact_wbvh).
+// higher depth-first rank, as trace_exact_wbvh).  (After an overflow, testing every slot of the
+// tree instead of the unfiltered walk saved registers but measured C4 f64 30 -> 52 ms: teapot rays
+// do overflow, and a wave then waits for 6 320 f64 tests.)
 template <typename R, int MAXD>
 __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<R>& sc, const Ray<R>& wray,
                                               HitMin<R, MAXD>& hm) {
@@ -1610,10 +1716,26 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
     uint32_t best_rank = 0;
     int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
     Ray<R> oray = wray;
+    // one candidate per trip, shifted down the list: an unrolled loop let the scheduler hoist the
+    // f64 primitive loads of all four at once (36 VGPRs of spills in the C5 / C4 f64 kernel)
+    int32_t cs[XCAND];
+    float cl[XCAND];
 #pragma unroll
     for (int j = 0; j < XCAND; ++j) {
-        if (c.cs[j] >= 0 && c.cl[j] <= c.bound) {
-            const DExactRef ref = sc.wexact[c.cs[j]];
+        cs[j] = c.cs[j];
+        cl[j] = c.cl[j];
+    }
+#pragma unroll 1
+    for (int j = 0; j < XCAND; ++j) {
+        const int32_t cj = cs[0];
+        const float lj = cl[0];
+#pragma unroll
+        for (int q = 0; q + 1 < XCAND; ++q) {
+            cs[q] = cs[q + 1];
+            cl[q] = cl[q + 1];
+        }
+        if (cj >= 0 && lj <= c.bound) {
+            const DExactRef ref = sc.wexact[cj];
             if (ref.inst != cur_inst) {  // the primitive's object-space ray (exact chain)
                 oray = wray;
                 if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
@@ -1638,9 +1760,9 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
 }
 
 // The prefilter over the world-BVH walk (RenderParams::exact_pf).
-template <typename R, int MAXD, int W = 0>
+template <typename R, int MAXD, int W = 0, bool LSTACK = false>
 __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                                    bool thread = false) {
+                                                    bool thread = false, uint16_t* lstk = nullptr) {
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
@@ -1655,6 +1777,23 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     if (W == XTHREAD_W || (W == 0 && thread)) {
         float cut = INFINITY;
         xthread_walk(sc, fr, cut, [&](int32_t ref) { offer_leaf(ref, cut); });
+    } else if constexpr (W == WBVH_COMPACT) {
+        WbvhTrav ts;
+        wbvh_begin(ts, wbvh_root(sc), fr);
+        auto walk = [&](auto& stk) {
+            while (true) {
+                while (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
+                if (ts.node == WBVH_DONE) break;
+                offer_leaf(ts.node, ts.t_best);
+                ts.node = wbvh4c_pop(ts, stk);
+            }
+        };
+        if constexpr (LSTACK) {
+            walk(lstk);
+        } else {
+            PrivStack16 stk;
+            walk(stk);
+        }
     } else {
         WbvhTrav ts;
         wbvh_begin(ts, wbvh_root(sc), fr);
@@ -1669,7 +1808,7 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
             ts.node = wbvh_pop(ts, stk);
         }
     }
-    if (c.over) return trace_exact_wbvh<R, MAXD, W>(sc, wray, hm, thread);
+    if (c.over) return trace_exact_wbvh<R, MAXD, W, true, LSTACK>(sc, wray, hm, thread, lstk);
     return xcands_finish(c, sc, wray, hm);
 }
 
@@ -1681,13 +1820,14 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
         static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
-        return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);
+        if constexpr (SIG::lstack) return trace_exact_wbvh_pf<R, MAXD, SIG::bvh, true>(sc, wray, hm, false, stack);
+        else return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);
     } else if constexpr (EXACT && sizeof(R) == 8) {
         const bool thread = sc.xthread != nullptr && xthread;
         if constexpr (PF) {  // plane-only scenes (KF_PLANES)
             if (exact_wbvh && pf) return trace_exact_wbvh_pf<R, MAXD>(sc, wray, hm, thread);
         }
-        if (exact_wbvh) return trace_exact_wbvh<R, MAXD>(sc, wray, hm, thread);
+        if (exact_wbvh) return trace_exact_wbvh<R, MAXD, 0, PF>(sc, wray, hm, thread);
         return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, all);
     } else return trace_bvh<R, MAXD, EXACT>(sc, wray, hm, EXACT && all);
 }
@@ -1700,7 +1840,7 @@ template <typename R, int MAXD, bool FLAT = false, bool STAGED = false>  // STAG
 __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, const Ray<R>& wray,
                                                      const HitMin<R, MAXD>& hm) {
     // hm.prim is always a primitive record: box and room hits name their face quad
-    const DPrimWorld<R> q = load16(STAGED ? (const DPrimWorld<R>*)((const unsigned char*)sc.wprims + hm.prim * WPRIM_LDS_STRIDE)
+    const DPrimWorld<R> q = load16(STAGED ? (const DPrimWorld<R>*)((const unsigned char*)sc.wprims + hm.prim * wprim_lds_stride(MAXD))
                                           : sc.wprims + hm.prim);
     R t = hm.t;  // world BVH: the closest key = t scaled by the winner's coplanar-tie factor (WCLASS_*)
     if (MAXD < 0 && (sc.wflags & WFLAG_COPLANAR)) {
@@ -1743,7 +1883,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
 
 // Instance mode: recomputed exactly as the candidate test computed it
 // (object-space point / normal / uv, then mapped out through the instances).
-template <typename R, int MAXD, bool EXACT>
+template <typename R, int MAXD, bool EXACT, bool PLANES = false>  // PLANES: no spheres (KF_PLANES)
 __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
     Ray<R> ray = wray;
     auto enter = [&](uint32_t iid) {
@@ -1781,7 +1921,8 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     }
     const DPrim<R>& pr = sc.prims[EXACT ? hm.prim : 0];
     if (!EXACT) {
-    } else if (pr.kind == PRIM_SPHERE) {  // sphere.rs:148-161
+    } else if (!PLANES && pr.kind == PRIM_SPHERE) {  // sphere.rs:148-161 (f64 acos / atan2: 50 VGPRs of
+                                                    // spills in the plane-only variant, were it compiled in)
         const V<R> center = ld3(pr.a) + ray.time * ld3(pr.b);
         h.p = ray.o + t * ray.d;
         outward = normalize(h.p - center);
@@ -1809,10 +1950,10 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     return h;
 }
 
-template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool STAGED = false>
+template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool STAGED = false, bool PLANES = false>
 __device__ __forceinline__ Rec<R> make_record(const DSceneView<R>& sc, const Ray<R>& wray, const HitMin<R, MAXD>& hm) {
     if constexpr (MAXD <= 0) return make_record_world<R, MAXD, FLAT, STAGED>(sc, wray, hm);
-    else return make_record_bvh<R, MAXD, EXACT>(sc, wray, hm);
+    else return make_record_bvh<R, MAXD, EXACT, PLANES>(sc, wray, hm);
 }
 
 // ----------------------------------------------------------------- shading
@@ -1887,6 +2028,9 @@ __device__ __forceinline__ double perlin_texture(const uint32_t* texels, const D
 // with the rounded reciprocal and one Markstein correction step, exact for all 256 values (the
 // product alone is 1 ulp off for 158 of them); explicit FMAs, so the exact kernel's
 // -ffp-contract=off build computes the same
+#ifndef NRT_TEX_FORMATS
+#define NRT_TEX_FORMATS 3  // image texel formats compiled in: 1 RGB32F, 2 RGBA8 (A/B via NRT_JIT_DEFS)
+#endif
 __device__ __forceinline__ float unorm8(uint32_t k) {
     constexpr float r = 1.0f / 255.0f;
     const float b = (float)k;
@@ -1919,7 +2063,8 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
             // reference (Q12): clamped to the last texel here.
             uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
             uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)t.b ? t.b - 1 : (uint32_t)fy);
-            if (t.format == TEXFMT_RGBA8) {  // one word (8 x 4 tiles): the three bytes, k / 255.0f exactly
+            if ((NRT_TEX_FORMATS & 2) && (!(NRT_TEX_FORMATS & 1) || t.format == TEXFMT_RGBA8)) {
+                // one word (8 x 4 tiles): the three bytes, k / 255.0f exactly
 #ifdef NRT_TEX_ROWMAJOR
                 const uint32_t w = sc.texels[t.offset + (uint64_t)y * t.a + x];
 #else
@@ -1959,7 +2104,7 @@ template <typename R> __device__ __forceinline__ R reflectance(R cosine, R ri) {
 
 // Copy the LDS-stageable scene arrays into dynamic LDS at `base` (all threads).
 template <typename R>
-__device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, unsigned char* base) {
+__device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, unsigned char* base, uint32_t wstride) {
     DSceneView<R> s = g;
     uint32_t off = 0;
     auto copy = [&](const void* src, uint32_t bytes) -> const void* {
@@ -1979,12 +2124,13 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
     s.fprims = (const DPrimFast<R>*)copy(g.fprims, g.n_fprims * (uint32_t)sizeof(DPrimFast<R>));
     s.inst_fast = (const DInstFast<R>*)copy(g.inst_fast, g.n_inst_fast * (uint32_t)sizeof(DInstFast<R>));
     s.mats_fast = (const DMatFast*)copy(g.mats_fast, g.n_mats_fast * (uint32_t)sizeof(DMatFast));
-    {  // world primitives WPRIM_LDS_STRIDE bytes apart (device_scene.hpp)
+    {  // world primitives wstride bytes apart (device_scene.hpp wprim_lds_stride)
         unsigned char* dst = base + off;
         const uint4* s4 = (const uint4*)g.wprims;
-        constexpr uint32_t Q = (uint32_t)sizeof(DPrimWorld<R>) / 16u, QS = WPRIM_LDS_STRIDE / 16u;
+        constexpr uint32_t Q = (uint32_t)sizeof(DPrimWorld<R>) / 16u;
+        const uint32_t QS = wstride / 16u;
         for (uint32_t k = threadIdx.x; k < g.n_wprims * Q; k += BLOCK) ((uint4*)dst)[(k / Q) * QS + k % Q] = s4[k];
-        off += (g.n_wprims * WPRIM_LDS_STRIDE + 15u) & ~15u;
+        off += (g.n_wprims * wstride + 15u) & ~15u;
         s.wprims = (const DPrimWorld<R>*)dst;
     }
     __syncthreads();
@@ -2032,6 +2178,9 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 #ifndef NRT_GRAB
 #define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
 #endif
+#ifndef NRT_PROBE_HEAD
+#define NRT_PROBE_HEAD 1  // skip queue heads a plain load shows empty before the atomic
+#endif
 #ifndef NRT_SLOTS_LIST
 #define NRT_SLOTS_LIST 2
 #endif
@@ -2047,7 +2196,7 @@ __host__ __device__ constexpr uint32_t philox_pool_bytes(uint32_t P) {
     return (BLOCK / 64) * philox_slots<MAXD>() * P * (3u * (uint32_t)sizeof(double) + 4u);
 }
 
-template <typename R, class G, int MAXD>
+template <typename R, class G, int MAXD, class SIG = NoSig>
 constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WORLD_LIST_WAVES
 #define NRT_WORLD_LIST_WAVES 6
@@ -2061,6 +2210,10 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_F64_SPHERE_WAVES
 #define NRT_F64_SPHERE_WAVES 3
 #endif
+#ifndef NRT_F64_LSTACK_WAVES
+#define NRT_F64_LSTACK_WAVES 3  // the LDS-stack variant: ring + stack + scene leave room for 3 workgroups
+#endif
+    if (sizeof(R) == 8 && SIG::lstack) return NRT_F64_LSTACK_WAVES;
     if (sizeof(R) == 8) return (kflags & KF_PLANES) ? NRT_F64_WAVES : NRT_F64_SPHERE_WAVES;
 #ifndef NRT_WBVH_WAVES
 #define NRT_WBVH_WAVES 1
@@ -2091,7 +2244,7 @@ template <bool COMPACT> struct StackEntry { using type = int32_t; };
 template <> struct StackEntry<true> { using type = uint16_t; };
 
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0, class SIG = NoSig>
-__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD>(KFLAGS)))
+__global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD, SIG>(KFLAGS)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     constexpr bool PROF = (KFLAGS & KF_PROF) != 0;
     constexpr bool PERLIN = (KFLAGS & KF_PERLIN) != 0;
@@ -2124,10 +2277,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
     // world-BVH stack (f32 kernels): the tree's bound + 1 entries (16-bit refs of the compact tree)
     using StackT = typename StackEntry<SIG::bvh == WBVH_COMPACT>::type;
-    const uint32_t stack_bytes = MAXD < 0 ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(StackT) : 0u;
+    const uint32_t stack_bytes =
+        (MAXD < 0 || SIG::lstack) ? (gsc.wbvh_stack + 1u) * BLOCK * (uint32_t)sizeof(StackT) : 0u;
     StackT* stack = stack_bytes ? (StackT*)(lds + ring_bytes + acc_bytes) + threadIdx.x : nullptr;
     DSceneView<R> sc = gsc;
-    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes);
+    if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes, wprim_lds_stride(MAXD));
 
     G g;
     // Camera vectors (camera.rs:205-227) q = 0..6: top_left, delta_u, delta_v, look_from,
@@ -2182,7 +2336,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             contrib = tp * cam(6);  // background
             return false;
         }
-        h = make_record<R, MAXD, EXACT, FLAT, LDS_SCENE>(sc, ray, hm);
+        h = make_record<R, MAXD, EXACT, FLAT, LDS_SCENE, (KFLAGS & KF_PLANES) != 0>(sc, ray, hm);
         m = material(h.mat);
         if (m.kind == MAT_DIFFUSE_LIGHT) {  // emit (diffuse_light.rs:62-75), no scatter
             const R k = bounced ? m.param : R(1.0);
@@ -2424,7 +2578,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
                         const uint32_t n = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS) - lo;
                         unsigned int* head = p.queue + x * QUEUE_STRIDE;
-                        if (n == 0 || __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n)
+                        if (n == 0 || (NRT_PROBE_HEAD && __hip_atomic_load(head, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT) >= n))
                             continue;
                         const uint32_t k = qk ? 1u : (uint32_t)NRT_GRAB;  // a steal takes one group
                         const uint32_t t = atomicAdd(head, k);

@@ -81,7 +81,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     // launch_variant), then the BVH stack
     const uint32_t ring = (G::uses_lds ? dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) : 0) +
                           (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
-    const uint32_t scene = lds_scene_bytes(v);
+    const uint32_t scene = lds_scene_bytes(v, MAXD);
     using dev::KF_FLAT;
     using dev::KF_PERLIN;
     using dev::KF_PROF;
@@ -106,6 +106,19 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                     using XT = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, dev::XTHREAD_W>;
                     if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XT>(p, v, ring + scene, stream);
                     else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XT>(p, v, ring, stream);
+                    return;
+                }
+                if (v.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
+                    using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
+                    const uint32_t stk = (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XL>(p, v, ring + stk + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XL>(p, v, ring + stk, stream);
+                    return;
+                }
+                if (v.wbvh4c) {  // the compact tree: 16-bit stack entries (half the scratch bytes)
+                    using XC = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT>;
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XC>(p, v, ring + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XC>(p, v, ring, stream);
                     return;
                 }
                 // (tree width left to the run time: fixing it measured C5 -0.3 %, C4 +2.8 %)

@@ -140,16 +140,22 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         const WorldBvh& xt = fs.exact_tree();
         const DBvhNode* xbn = wbn;
         const DBvh4Node* xb4 = wb4;
+        const DBvh4cNode* xb4c = wb4c;
         if (&xt != &fs.wbvh) {
             xbn = (DBvhNode*)track(upload(xt.nodes, "wbvh_x"), xt.nodes.size() * sizeof(DBvhNode));
             xb4 = (DBvh4Node*)track(upload(xt.nodes4, "wbvh4_x"), xt.nodes4.size() * sizeof(DBvh4Node));
+            xb4c = (DBvh4cNode*)track(upload(xt.nodes4c, "wbvh4c_x"), xt.nodes4c.size() * sizeof(DBvh4cNode));
         }
+        // exact walk on the compact tree (16-bit stack entries) unless NRT_EXACT_COMPACT=0
+        const char* xce = std::getenv("NRT_EXACT_COMPACT");
+        const bool x4c = !xt.nodes4c.empty() && !(xce && xce[0] == '0');
         const bool x4 = !xt.nodes4.empty() && use_wbvh4(fs);
         auto* xth = (DThreadNode*)track(upload(xt.threaded, "wbvh_threaded"), xt.threaded.size() * sizeof(DThreadNode));
         ds->v64 = DSceneView<double>{n64, p64, x64, inst, mats, texs, texels, fs.root, fs.max_depth,
                                      (uint32_t)fs.nodes.size(), np, nx, ni, nm, nt, nullptr, nullptr, nullptr, 0, 0, 0,
                                      nullptr, 0, nullptr, 0, 0, wx_ok ? xbn : nullptr,
-                                     (wx_ok && x4) ? xb4 : nullptr, nullptr, xt.root4, xt.root,
+                                     (wx_ok && x4) ? xb4 : nullptr, (wx_ok && x4 && x4c) ? xb4c : nullptr,
+                                     xt.root4, xt.root,
                                      wx_ok ? (uint32_t)xt.nodes.size() : 0u,
                                      std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? xth : nullptr,
                                      wx_ok ? xt.threaded_n : 0u, wx_ok ? wx : nullptr,
@@ -169,7 +175,8 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         ds->flat = !ds->perlin;
         for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
         // unit kinds from the runs (box / room units also hold header and empty face slots)
-        for (uint32_t run : fs.wruns) ds->flat &= (run & WRUN_KIND_MASK) != PRIM_SPHERE;
+        for (uint32_t run : fs.wruns)
+            ds->flat &= (run & WRUN_KIND_MASK) != PRIM_SPHERE && (run & WRUN_KIND_MASK) != PRIM_SPHERE32;
         ds->flat &= !fs.wruns.empty();
         ds->wbvh_prims = wbp;
         const size_t qbytes = (size_t)QUEUE_SLOTS * QUEUE_HEADS * QUEUE_STRIDE * sizeof(unsigned int);
@@ -266,7 +273,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         // width and tie flag, as template arguments; the same LDS layout as launch_one
         void* jit = nullptr;
         uint32_t stack_entry = 4;  // bytes per world-BVH stack entry of the kernel launched
-        const uint32_t scene_lds = lds_scene_bytes(v);
+        const uint32_t scene_lds = lds_scene_bytes(v, maxd);
         const bool staged = scene_lds <= LDS_SCENE_LIMIT;
         const uint32_t lds_fixed = staged ? scene_lds : 0u;  // (+ the BVH stack: launch_fast_jit)
         if ((maxd == MODE_WORLD_LIST || maxd == MODE_WORLD_BVH) && (rng == RNG_PHILOX || rng == RNG_CHACHA8) &&

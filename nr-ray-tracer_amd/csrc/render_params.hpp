@@ -45,11 +45,9 @@ struct RenderParams {
     double acc_scale, acc_unscale;  // 2^k, 2^-k
     uint32_t groups;                // Philox: pixel groups (of wave_pixels) in this launch
     // Philox: QUEUE_HEADS group-queue heads, QUEUE_STRIDE words apart (device, zeroed
-    // before the launch); head x hands out the dynamic part of the x-th contiguous eighth of
-    // the groups, whose first static_share / 1024 (in whole rounds) the waves of label x take
-    // round-robin without an atomic (kernel.hpp, Philox branch).
+    // before the launch); head x hands out the x-th contiguous eighth of the groups
+    // (kernel.hpp, Philox branch).
     unsigned int* queue;
-    uint32_t static_share;
     uint32_t width, height;
     uint32_t spp;
     uint32_t max_bounces;
@@ -75,6 +73,9 @@ struct RenderParams {
     // Exact world mode: the stackless threaded walk of the culling tree (kernel.hpp xthread_walk)
     // instead of the 4-wide walk with a private stack.
     uint32_t exact_thread;
+    // Exact world mode on the compact tree: its traversal stack in LDS (16-bit entries) and
+    // 3 waves per SIMD, instead of a private (scratch) stack at 4 (ExactSig lstack).
+    uint32_t exact_lstack;
     float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
 };
 

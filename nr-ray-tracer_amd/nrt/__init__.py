@@ -149,6 +149,9 @@ def lib() -> C.CDLL:
             raise NrtError(-3, f"{LIB_PATH} not built: run __graft_entry__.build() / make -C nr-ray-tracer_amd")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            # an A/B build named by NRT_LIB (scripts/ab_configs.py) may predate newer entry points
+            if os.environ.get("NRT_LIB") and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -358,7 +361,10 @@ class Scene:
         h = C.c_void_p()
         cam = _Camera()
         ov = C.byref(overrides._c()) if overrides is not None else None
-        _check(lib().nrt_scene_load_ex(os.fsencode(path), ov, 1 if legacy_schema else 0, C.byref(h), C.byref(cam)))
+        if legacy_schema:
+            _check(lib().nrt_scene_load_ex(os.fsencode(path), ov, 1, C.byref(h), C.byref(cam)))
+        else:
+            _check(lib().nrt_scene_load(os.fsencode(path), ov, C.byref(h), C.byref(cam)))
         return Scene(h.value, Camera._from_c(cam))
 
     def close(self) -> None:

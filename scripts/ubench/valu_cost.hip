@@ -42,6 +42,16 @@ DEF_OP(v_bitop3_b32, uint32_t, i * 2654435761u, asm volatile("v_bitop3_b32 %0, %
 DEF_OP(v_cndmask_b32, uint32_t, i, asm volatile("v_cmp_gt_u32 vcc, %1, %0\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(a) : "v"(b) : "vcc"))
 DEF_OP(v_rcp_f32, float, 1.0f + i * 1e-7f, asm volatile("v_rcp_f32 %0, %0" : "+v"(a)))
 DEF_OP(v_exp_f32, float, i * 1e-9f, asm volatile("v_exp_f32 %0, %0" : "+v"(a)))
+// round 3: the 4-wide node decode candidates (byte -> float conversions vs f16 mixes)
+DEF_OP(v_cvt_f32_ubyte1, uint32_t, i, asm volatile("v_cvt_f32_ubyte1 %0, %0" : "+v"(a)))
+DEF_OP(v_fma_mix_f32, float, 1.0f + i * 1e-7f, asm volatile("v_fma_mix_f32 %0, %1, %0, %0 op_sel_hi:[1,0,0]" : "+v"(a) : "v"(b)))
+DEF_OP(v_perm_b32, uint32_t, i * 2654435761u, asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(a) : "v"(b)))
+DEF_OP(v_max3_f32, float, 1.0f + i * 1e-7f, asm volatile("v_max3_f32 %0, %1, %0, %1" : "+v"(a) : "v"(b)))
+DEF_OP(v_min_f32, float, 1.0f + i * 1e-7f, asm volatile("v_min_f32 %0, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_pk_add_f32, f32x2, (f32x2{1.0f, 2.0f}), asm volatile("v_pk_add_f32 %0, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_pk_mul_f32, f32x2, (f32x2{1.0f, 2.0f}), asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(a) : "v"(b)))
+DEF_OP(v_fmac_f32, float, 1.0f + i * 1e-7f, asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(a) : "v"(b)))
+DEF_OP(v_cvt_f32_f16, uint32_t, i, asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(a)))
 
 template <class Op>
 __global__ void __launch_bounds__(256) bench(uint64_t* out, uint32_t* sink) {
@@ -135,5 +145,14 @@ int main() {
     run<v_cndmask_b32>(cus);
     run<v_rcp_f32>(cus);
     run<v_exp_f32>(cus);
+    run<v_cvt_f32_ubyte1>(cus);
+    run<v_fma_mix_f32>(cus);
+    run<v_perm_b32>(cus);
+    run<v_max3_f32>(cus);
+    run<v_min_f32>(cus);
+    run<v_pk_add_f32>(cus);
+    run<v_pk_mul_f32>(cus);
+    run<v_fmac_f32>(cus);
+    run<v_cvt_f32_f16>(cus);
     return 0;
 }
