@@ -2179,7 +2179,12 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 #define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
 #endif
 #ifndef NRT_PROBE_HEAD
-#define NRT_PROBE_HEAD 1  // skip queue heads a plain load shows empty before the atomic
+// 1: skip queue heads an agent-scope load shows empty before the atomic (saved C5 ~2 MB of HBM
+// writes, but the extra round trip before each fetch cost C3 earth 6.67 -> 7.32 ms): off
+#define NRT_PROBE_HEAD 0
+#endif
+#ifndef NRT_FETCH_AHEAD
+#define NRT_FETCH_AHEAD 64u  // Philox: take the next group when fewer samples are left to claim
 #endif
 #ifndef NRT_SLOTS_LIST
 #define NRT_SLOTS_LIST 2
@@ -2393,13 +2398,45 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     };
 
     if constexpr (G::exact_stream) {
-        const uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
-        if (i >= p.pixel_end) return;
-        const uint32_t x = i % p.width;
-        const uint32_t y = p.row_offset + (i / p.width) * p.row_stride;
-        g.init((uint64_t)y * p.width + x, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);  // stream (camera.rs:320-323)
+        // Persistent lanes: the grid holds as many workgroups as stay resident, each lane renders
+        // pixel after pixel (its samples in order, as the reference), and a lane whose pixel is
+        // done takes the next one from a counter (p.queue[0]; one atomic per wave and refill), so
+        // no lane idles while its wave's slowest pixel finishes: pixels differ widely in path work
+        // (a light's pixels end every path at once), and a wave used to run to its slowest pixel.
+        // A pixel's result depends on its index alone (its ChaCha8 stream, its sample order).
+        uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
+        bool have = i < p.pixel_end;
+        uint32_t x = 0, y = 0;
         double ax = 0.0, ay = 0.0, az = 0.0;
         uint32_t s = 0;  // next sample of the pixel
+        auto start_pixel = [&]() {
+            x = i % p.width;
+            y = p.row_offset + (i / p.width) * p.row_stride;
+            g.init((uint64_t)y * p.width + x, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);  // stream (camera.rs:320-323)
+            ax = ay = az = 0.0;
+            s = 0;
+        };
+        auto finish_pixel = [&]() {
+            const double spp = (double)p.spp;
+            float* o = p.out + 3ull * i;
+            o[0] = (float)(ax / spp);
+            o[1] = (float)(ay / spp);
+            o[2] = (float)(az / spp);
+        };
+        const uint32_t dyn0 = p.pixel_begin + gridDim.x * BLOCK;  // first pixel handed out by the counter
+        auto next_pixel = [&](bool need) -> bool {                 // uniform; true: this lane got a pixel
+            const uint64_t m = __ballot(need);
+            if (m == 0ull) return false;
+            uint32_t base = 0;
+            if (leader()) base = atomicAdd(p.queue, (uint32_t)__popcll(m));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (!need) return false;
+            i = dyn0 + base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            have = i < p.pixel_end;
+            if (have) start_pixel();
+            return have;
+        };
+        if (have) start_pixel();
 
         // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
         auto camera_ray = [&]() -> bool {
@@ -2454,7 +2491,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             // start their next segment (active-ray compaction within the wave).
             static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
             WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            bool active = camera_ray();
+            bool active = have && camera_ray();
             auto begin = [&]() {
                 // depth cap: no query, the lane waits to be shaded as black (Q6)
                 wbvh_begin(ts, b < p.max_bounces ? wbvh_root(gsc) : WBVH_DONE, ray);
@@ -2486,14 +2523,25 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         atomicAdd(&prof[wave][3], t2 - t1);
                     }
                 }
+                const bool done = have && !active;  // the pixel's last sample has ended
+                if (done) finish_pixel();
+                if (next_pixel(done)) {
+                    active = camera_ray();
+                    begin();
+                }
                 if (__ballot(active) == 0ull) break;
             }
         } else {
             bool fresh = true;
             while (true) {
+                const bool done = have && fresh && s >= p.spp;  // the pixel's last sample has ended
+                if (done) finish_pixel();
+                next_pixel(done);
+                if (__ballot(have) == 0ull) break;
+                if (!have) continue;
                 const unsigned long long t0 = stamp();
                 if (fresh) {
-                    if (!camera_ray()) break;
+                    camera_ray();  // (s < spp: a sample is left)
                     fresh = false;
                 }
                 const unsigned long long t1 = stamp();
@@ -2521,11 +2569,6 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
         }
         flush_prof();
-        const double spp = (double)p.spp;
-        float* o = p.out + 3ull * i;
-        o[0] = (float)(ax / spp);
-        o[1] = (float)(ay / spp);
-        o[2] = (float)(az / spp);
     } else {
         // ------------------------------------------------ Philox: per-wave sample pool
         // Persistent waves.  A wave takes groups of P consecutive pixels from a global
@@ -2681,8 +2724,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 }
             }
             if constexpr (NS == 2) {
-                if (!exhausted && !ready && GS - next < 64u && (cs ? gids[0] : gids[1]) == NO_GROUP) fetch(cs ^ 1u);
-            } else if (!exhausted && !ready && GS - next < 64u) {
+                if (!exhausted && !ready && GS - next < NRT_FETCH_AHEAD && (cs ? gids[0] : gids[1]) == NO_GROUP) fetch(cs ^ 1u);
+            } else if (!exhausted && !ready && GS - next < NRT_FETCH_AHEAD) {
                 const uint32_t r = (cs + 1u) & (NS - 1u);
                 bool free = false;
 #pragma unroll

@@ -41,9 +41,11 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
             throw std::runtime_error("HIP error in hipModuleLaunchKernel (scene-specialised kernel)");
     };
     const uint32_t stack = maxd == MODE_WORLD_BVH ? (v.wbvh_stack + 1u) * dev::BLOCK * stack_entry : 0u;
-    if (rng == RNG_CHACHA8) {  // one lane per pixel (launch_variant): ring + stack below the staged scene
+    if (rng == RNG_CHACHA8) {  // persistent lanes (launch_variant): ring + stack below the staged scene
         const uint32_t npix = p0.pixel_end - p0.pixel_begin;
-        launch((npix + dev::BLOCK - 1) / dev::BLOCK, lds_fixed + dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) + stack, p0);
+        const uint32_t lds = lds_fixed + dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) + stack;
+        const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
+        launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(need, resident(lds))), lds, p0);
         return;
     }
     if (maxd == MODE_WORLD_BVH)  // below the staged scene: the traversal stack (launch_one's ring)

@@ -63,8 +63,10 @@ template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS,
 static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint32_t lds_fixed, hipStream_t stream) {
     auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, KFLAGS, SIG>;
     const uint32_t npix = p0.pixel_end - p0.pixel_begin;
-    if constexpr (G::exact_stream) {
-        hipLaunchKernelGGL(kernel, dim3((npix + dev::BLOCK - 1) / dev::BLOCK), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
+    if constexpr (G::exact_stream) {  // persistent lanes (render_kernel): the resident workgroups at most
+        const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
+        const uint64_t blocks = std::max<uint64_t>(1, std::min(need, resident_blocks(kernel, lds_fixed)));
+        hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
     } else {
         philox_launch<MAXD>(
             p0, lds_fixed, [&](uint32_t lds) { return resident_blocks(kernel, lds); },

@@ -248,7 +248,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     DeviceGuard guard(ds->device);  // memset, occupancy query and launch on the scene's device
     hipStream_t stream = (hipStream_t)stream_ptr;
     RenderParams q = p;
-    if (rng == RNG_PHILOX) {  // group size and count: launch_variant (launch_impl.hpp)
+    {  // Philox: group queue heads; ChaCha8: the pixel counter of the persistent lanes (head 0)
         const size_t qwords = (size_t)QUEUE_HEADS * QUEUE_STRIDE;
         q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;
         check(hipMemsetAsync(q.queue, 0, qwords * sizeof(unsigned int), stream), "hipMemsetAsync(queue)");

@@ -46,7 +46,8 @@ struct RenderParams {
     uint32_t groups;                // Philox: pixel groups (of wave_pixels) in this launch
     // Philox: QUEUE_HEADS group-queue heads, QUEUE_STRIDE words apart (device, zeroed
     // before the launch); head x hands out the x-th contiguous eighth of the groups
-    // (kernel.hpp, Philox branch).
+    // (kernel.hpp, Philox branch).  ChaCha8: word 0 counts the pixels handed out past the
+    // grid's first round (persistent lanes).
     unsigned int* queue;
     uint32_t width, height;
     uint32_t spp;

@@ -8,8 +8,9 @@ C4="--scene scenes/utah-teapot-scene.json"; C3="--scene scenes/earth.toml --widt
 C5X="--precision f64 --rng chacha8 --spp 64"; C4X="$C4 --precision f64 --rng chacha8 --spp 16"
 AB="timeout -k 10 900 python scripts/ab_configs.py --reps 2"
 BASE=nr-ray-tracer_amd/ab/base/libnrt.so; NEW=nr-ray-tracer_amd/nrt/libnrt.so
-$AB --out gpurun_out/${tag}_c4.jsonl --lib f62b=nr-ray-tracer_amd/ab/f62b/libnrt.so --lib new=$NEW --cfg c4="$C4" || exit 1
-$AB --out gpurun_out/${tag}_c3.jsonl --lib base=$BASE --lib new=$NEW --env def="" --env off="NRT_TEX_RGBA8=0 NRT_SPHERE_F32=0 NRT_JIT_DEFS=-DNRT_SPHERE_REPROJ=0" --env off1="NRT_TEX_RGBA8=0 NRT_SPHERE_F32=0 NRT_JIT_DEFS='-DNRT_SPHERE_REPROJ=0 -DNRT_TEX_FORMATS=1'" --env off1np="NRT_TEX_RGBA8=0 NRT_SPHERE_F32=0 NRT_JIT_DEFS='-DNRT_SPHERE_REPROJ=0 -DNRT_TEX_FORMATS=1 -DNRT_PROBE_HEAD=0'" --env def2="NRT_JIT_DEFS=-DNRT_TEX_FORMATS=2" --cfg c3="$C3" || exit 1
+PREV=nr-ray-tracer_amd/ab/prev/libnrt.so
+$AB --out gpurun_out/${tag}_x.jsonl --lib prev=$PREV --lib new=$NEW --cfg c5x="$C5X" --cfg c4x="$C4X" --cfg c5c="--rng chacha8 --spp 64" || exit 1
+$AB --out gpurun_out/${tag}_fa.jsonl --lib new=$NEW --env def="" --env fa128="NRT_JIT_DEFS=-DNRT_FETCH_AHEAD=128u" --env fa256="NRT_JIT_DEFS=-DNRT_FETCH_AHEAD=256u" --cfg c3="$C3" --cfg c5="" --cfg c4="$C4" || exit 1
 pmc() {  # name lib counters bench-args...
   local n=$1 lib=$2 c=$3; shift 3
   env NRT_LIB=$PWD/$lib timeout -s KILL 180 rocprofv3 --pmc $c -d gpurun_out/${tag}_pmc_$n -o run --output-format csv -- python3 bench.py --no-cpu-baseline --kernel-only --steps 2 --warmup 1 "$@" > /dev/null 2> gpurun_out/${tag}_pmc_$n.err || { echo "pmc $n failed"; tail -3 gpurun_out/${tag}_pmc_$n.err; exit 1; }
