@@ -244,7 +244,10 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // slower than the 4-wide walk with its private stack: C5 f64 spp 64 69.2 vs 57.7 ms, C4 128.3 vs 98.6
     p.exact_thread = 0;
     if (const char* e = std::getenv("NRT_EXACT_THREAD")) p.exact_thread = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
-    p.exact_lstack = 0;  // knob NRT_EXACT_LSTACK=1: the compact walk's stack in LDS at 3 waves per SIMD
+    // the compact walk's stack in LDS at 3 waves per SIMD (no scratch traffic: C5 f64 6.1 GB -> 57 MB
+    // of HBM writes at spp 64) rather than in scratch at 4: with persistent lanes the two run even
+    // (C5 f64 54.9 / 55.0 ms, C4 15.2 / 14.7 ms); knob NRT_EXACT_LSTACK=0 for the scratch stack
+    p.exact_lstack = 1;
     if (const char* e = std::getenv("NRT_EXACT_LSTACK")) p.exact_lstack = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;

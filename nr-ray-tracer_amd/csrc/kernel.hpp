@@ -2400,10 +2400,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     if constexpr (G::exact_stream) {
         // Persistent lanes: the grid holds as many workgroups as stay resident, each lane renders
         // pixel after pixel (its samples in order, as the reference), and a lane whose pixel is
-        // done takes the next one from a counter (p.queue[0]; one atomic per wave and refill), so
-        // no lane idles while its wave's slowest pixel finishes: pixels differ widely in path work
-        // (a light's pixels end every path at once), and a wave used to run to its slowest pixel.
-        // A pixel's result depends on its index alone (its ChaCha8 stream, its sample order).
+        // done takes the next one, so no lane idles while its wave's slowest pixel finishes:
+        // pixels differ widely in path work (a light's pixels end every path at once), and a
+        // wave used to run to its slowest pixel (C4 f64 28.7 -> 15.6 ms at spp 16).  The pixels
+        // past the grid's first round come from per-XCD counters over contiguous eighths of them
+        // (as the Philox groups: an XCD's waves work on one image region, whose texels and nodes
+        // its L2 then holds; one global counter cost the textured earth 4 %), one atomic per wave
+        // and refill.  A pixel's result depends on its index alone (its ChaCha8 stream and
+        // sample order), never on which lane ran it.
         uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
         bool have = i < p.pixel_end;
         uint32_t x = 0, y = 0;
@@ -2423,18 +2427,40 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             o[1] = (float)(ay / spp);
             o[2] = (float)(az / spp);
         };
-        const uint32_t dyn0 = p.pixel_begin + gridDim.x * BLOCK;  // first pixel handed out by the counter
-        auto next_pixel = [&](bool need) -> bool {                 // uniform; true: this lane got a pixel
+        const uint32_t dyn0 = p.pixel_begin + gridDim.x * BLOCK;  // first pixel handed out by the counters
+        const uint32_t ndyn = p.pixel_end > dyn0 ? p.pixel_end - dyn0 : 0u;
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        uint32_t qk = 0;  // counters found exhausted (wave-uniform; QUEUE_HEADS: no pixel left)
+        auto next_pixel = [&](bool need) -> bool {  // uniform; true: this lane got a pixel
             const uint64_t m = __ballot(need);
-            if (m == 0ull) return false;
-            uint32_t base = 0;
-            if (leader()) base = atomicAdd(p.queue, (uint32_t)__popcll(m));
+            if (m == 0ull || qk >= QUEUE_HEADS) return false;
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            uint32_t base = 0, grant = 0;
+            if (leader()) {
+                for (; qk < QUEUE_HEADS; ++qk) {
+                    const uint32_t xh = (xcc + qk) & (QUEUE_HEADS - 1u);
+                    const uint32_t lo = (uint32_t)((uint64_t)xh * ndyn / QUEUE_HEADS);
+                    const uint32_t n = (uint32_t)((uint64_t)(xh + 1u) * ndyn / QUEUE_HEADS) - lo;
+                    if (n == 0) continue;
+                    const uint32_t t = atomicAdd(p.queue + xh * QUEUE_STRIDE, cnt);
+                    if (t < n) {
+                        base = lo + t;
+                        grant = min(cnt, n - t);
+                        break;
+                    }
+                }
+            }
             base = __builtin_amdgcn_readfirstlane(base);
+            grant = __builtin_amdgcn_readfirstlane(grant);
+            qk = __builtin_amdgcn_readfirstlane(qk);
             if (!need) return false;
-            i = dyn0 + base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            have = i < p.pixel_end;
-            if (have) start_pixel();
-            return have;
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (rank >= grant) return false;  // (the next round asks again)
+            i = dyn0 + base + rank;
+            have = true;
+            start_pixel();
+            return true;
         };
         if (have) start_pixel();
 
@@ -2523,9 +2549,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         atomicAdd(&prof[wave][3], t2 - t1);
                     }
                 }
-                const bool done = have && !active;  // the pixel's last sample has ended
-                if (done) finish_pixel();
-                if (next_pixel(done)) {
+                if (have && !active) {  // the pixel's last sample has ended
+                    finish_pixel();
+                    have = false;
+                }
+                if (next_pixel(!have)) {
                     active = camera_ray();
                     begin();
                 }
@@ -2534,10 +2562,12 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         } else {
             bool fresh = true;
             while (true) {
-                const bool done = have && fresh && s >= p.spp;  // the pixel's last sample has ended
-                if (done) finish_pixel();
-                next_pixel(done);
-                if (__ballot(have) == 0ull) break;
+                if (have && fresh && s >= p.spp) {  // the pixel's last sample has ended
+                    finish_pixel();
+                    have = false;
+                }
+                next_pixel(!have);
+                if (__ballot(have) == 0ull) break;  // (no lane holds a pixel: the counters are exhausted)
                 if (!have) continue;
                 const unsigned long long t0 = stamp();
                 if (fresh) {

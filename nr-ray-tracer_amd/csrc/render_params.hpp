@@ -75,7 +75,7 @@ struct RenderParams {
     // instead of the 4-wide walk with a private stack.
     uint32_t exact_thread;
     // Exact world mode on the compact tree: its traversal stack in LDS (16-bit entries) and
-    // 3 waves per SIMD, instead of a private (scratch) stack at 4 (ExactSig lstack).
+    // 3 waves per SIMD (default), or a private (scratch) stack at 4 (ExactSig lstack).
     uint32_t exact_lstack;
     float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
 };

@@ -9,10 +9,11 @@ C5X="--precision f64 --rng chacha8 --spp 64"; C4X="$C4 --precision f64 --rng cha
 AB="timeout -k 10 900 python scripts/ab_configs.py --reps 2"
 BASE=nr-ray-tracer_amd/ab/base/libnrt.so; NEW=nr-ray-tracer_amd/nrt/libnrt.so
 PREV=nr-ray-tracer_amd/ab/prev/libnrt.so
-$AB --out gpurun_out/${tag}_x.jsonl --lib prev=$PREV --lib new=$NEW --cfg c5x="$C5X" --cfg c4x="$C4X" --cfg c5c="--rng chacha8 --spp 64" || exit 1
-$AB --out gpurun_out/${tag}_fa.jsonl --lib new=$NEW --env def="" --env fa128="NRT_JIT_DEFS=-DNRT_FETCH_AHEAD=128u" --env fa256="NRT_JIT_DEFS=-DNRT_FETCH_AHEAD=256u" --cfg c3="$C3" --cfg c5="" --cfg c4="$C4" || exit 1
+$AB --out gpurun_out/${tag}_x.jsonl --lib prev=$PREV --lib new=$NEW --cfg c3x="$C3 --precision f64 --rng chacha8 --spp 16" --cfg c5x="$C5X" --cfg c4x="$C4X" --cfg c5c="--rng chacha8 --spp 64" || exit 1
 pmc() {  # name lib counters bench-args...
   local n=$1 lib=$2 c=$3; shift 3
   env NRT_LIB=$PWD/$lib timeout -s KILL 180 rocprofv3 --pmc $c -d gpurun_out/${tag}_pmc_$n -o run --output-format csv -- python3 bench.py --no-cpu-baseline --kernel-only --steps 2 --warmup 1 "$@" > /dev/null 2> gpurun_out/${tag}_pmc_$n.err || { echo "pmc $n failed"; tail -3 gpurun_out/${tag}_pmc_$n.err; exit 1; }
 }
+pmc c5x_def $NEW "WRITE_SIZE SQ_WAVES" $C5X
+pmc c4x_def $NEW "WRITE_SIZE SQ_WAVES" $C4X
 echo done
