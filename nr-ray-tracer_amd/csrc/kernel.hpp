@@ -185,14 +185,22 @@ struct ChaCha8 {
         }
         count += 8;
     }
-    __device__ __forceinline__ uint64_t next() {
-        if (__ballot(count == 0) != 0ull) {
+    // At least k (<= 8) words in every active lane's ring: one ballot (and at most one
+    // refill site) for a sampler's k draws instead of one per draw.  Same words, same order.
+    __device__ __forceinline__ void ensure(uint32_t k) {
+        if (__ballot(count < k) != 0ull) {
             if (count <= RING - 8) refill();
         }
+    }
+    __device__ __forceinline__ uint64_t take() {  // the next word; ensure() made it present
         const uint2 v = ring[head * BLOCK];
         head = (head + 1) & (RING - 1);
         --count;
         return (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
+    __device__ __forceinline__ uint64_t next() {
+        ensure(1);
+        return take();
     }
 };
 
@@ -312,6 +320,8 @@ struct Philox {
         const uint32_t lo = next32();
         return (uint64_t)lo | ((uint64_t)next32() << 32);
     }
+    __device__ __forceinline__ void ensure(uint32_t) {}
+    __device__ __forceinline__ uint64_t take() { return next(); }
     // Render loop: one whole block per lane per iteration, keyed by (pixel, sample,
     // step): step 0 = camera ray, b + 1 = scatter at bounce b, defocus_step() = the
     // camera's second block when the defocus disk is on.  The draws are w.x, w.y, w.z.
@@ -368,13 +378,20 @@ __device__ __forceinline__ R draw(G& g, R low, R high) {
         return Uniform<R>::range(g.next(), low, high);
     }
 }
+// A draw whose word g.ensure() already provided (ChaCha8: no per-draw ballot).
+template <typename R, class G>
+__device__ __forceinline__ R draw_taken(G& g, R low, R high) {
+    if constexpr (sizeof(R) == 4 && !G::uses_lds) return draw<R>(g, low, high);
+    else return Uniform<R>::range(g.take(), low, high);
+}
 
 // vector.rs:61-70 — rejection in [-1,1)^3 until 1e-160 < |p|^2 <= 1, returns p/|p|^2
 template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sphere(G& g) {
     while (true) {
-        const R x = draw<R>(g, R(-1), R(1));
-        const R y = draw<R>(g, R(-1), R(1));
-        const R z = draw<R>(g, R(-1), R(1));
+        g.ensure(3);
+        const R x = draw_taken<R>(g, R(-1), R(1));
+        const R y = draw_taken<R>(g, R(-1), R(1));
+        const R z = draw_taken<R>(g, R(-1), R(1));
         const V<R> p = mk(x, y, z);
         const R ls = dot(p, p);
         const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
@@ -384,8 +401,9 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sp
 // vector.rs:72-81 — rejection in [-1,1)^2 until |p|^2 < 1, returns p/|p|^2
 template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_disk(G& g) {
     while (true) {
-        const R x = draw<R>(g, R(-1), R(1));
-        const R y = draw<R>(g, R(-1), R(1));
+        g.ensure(2);
+        const R x = draw_taken<R>(g, R(-1), R(1));
+        const R y = draw_taken<R>(g, R(-1), R(1));
         const V<R> p = mk(x, y, R(0));
         const R ls = dot(p, p);
         if (ls < R(1)) return vdiv(p, ls);
@@ -1627,6 +1645,9 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
 // at the bound raised by 2^-20 as there.  A lane with more than XCAND live candidates at once
 // (never seen on the reference scenes) falls back to trace_exact_wbvh.
 constexpr int XCAND = 4;
+#ifndef NRT_EXACT_IFIF
+#define NRT_EXACT_IFIF 0  // the prefiltered compact walk as if-if trips (A/B build)
+#endif
 __device__ __forceinline__ float absdot(V<float> a, V<float> b) {
     return fabsf(a.x * b.x) + fabsf(a.y * b.y) + fabsf(a.z * b.z);
 }
@@ -1781,12 +1802,31 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
         WbvhTrav ts;
         wbvh_begin(ts, wbvh_root(sc), fr);
         auto walk = [&](auto& stk) {
+#if NRT_EXACT_IFIF
+            // if-if trips: one node visit or one primitive offer per lane per trip
+            int32_t leaf = WBVH_NO_LEAF;  // leaf cursor ~(first << 3 | more)
+            while (true) {
+                if (leaf != WBVH_NO_LEAF) {
+                    const uint32_t v = ~(uint32_t)leaf, first = v >> 3, more = v & 7u;
+                    if (c.offer(load16(sc.wxprims + first), fr, first)) ts.t_best = c.bound * (1.0f + 0x1p-20f);
+                    leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+                } else if (ts.node >= 0) {
+                    wbvh4c_visit<R>(ts, sc, stk);
+                }
+                if (leaf == WBVH_NO_LEAF && ts.node < 0) {
+                    if (ts.node == WBVH_DONE) break;
+                    leaf = ts.node;
+                    ts.node = wbvh4c_pop(ts, stk);
+                }
+            }
+#else
             while (true) {
                 while (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
                 if (ts.node == WBVH_DONE) break;
                 offer_leaf(ts.node, ts.t_best);
                 ts.node = wbvh4c_pop(ts, stk);
             }
+#endif
         };
         if constexpr (LSTACK) {
             walk(lstk);
@@ -2471,8 +2511,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             ++s;
             R ox = R(0), oy = R(0);
             if (p.spp > 1) {
-                ox = draw<R>(g, R(-0.5), R(0.5));
-                oy = draw<R>(g, R(-0.5), R(0.5));
+                g.ensure(2);
+                ox = draw_taken<R>(g, R(-0.5), R(0.5));
+                oy = draw_taken<R>(g, R(-0.5), R(0.5));
             }
             const V<R> point = (cam(0) + ((R)x + ox) * cam(1)) + ((R)y + oy) * cam(2);
             const V<R> disk = random_in_unit_disk<R>(g);

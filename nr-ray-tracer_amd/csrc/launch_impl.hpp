@@ -104,29 +104,34 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
     if constexpr (sizeof(R) == 8 && MAXD == 1 && G::exact_stream) {
         if (planes && !perlin && !p.counters) {  // KF_PLANES: the 4-wave f64 variant
             if (p.exact_wbvh && p.exact_pf && !p.exact_all) {  // the prefiltered world walk only
-                if (p.exact_thread && v.xthread) {  // the stackless threaded walk
+                // (the world walk never reads the reference node array: not staged, 2.4 KB of
+                // LDS for the Cornell box)
+                DSceneView<R> vw = v;
+                vw.n_nodes = 0;
+                const uint32_t scene = lds_scene_bytes(vw, MAXD);
+                if (p.exact_thread && vw.xthread) {  // the stackless threaded walk
                     using XT = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, dev::XTHREAD_W>;
-                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XT>(p, v, ring + scene, stream);
-                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XT>(p, v, ring, stream);
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XT>(p, vw, ring + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XT>(p, vw, ring, stream);
                     return;
                 }
-                if (v.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
+                if (vw.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
                     using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
-                    const uint32_t stk = (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
-                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XL>(p, v, ring + stk + scene, stream);
-                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XL>(p, v, ring + stk, stream);
+                    const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XL>(p, vw, ring + stk + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XL>(p, vw, ring + stk, stream);
                     return;
                 }
-                if (v.wbvh4c) {  // the compact tree: 16-bit stack entries (half the scratch bytes)
+                if (vw.wbvh4c) {  // the compact tree: 16-bit stack entries (half the scratch bytes)
                     using XC = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT>;
-                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XC>(p, v, ring + scene, stream);
-                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XC>(p, v, ring, stream);
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XC>(p, vw, ring + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XC>(p, vw, ring, stream);
                     return;
                 }
                 // (tree width left to the run time: fixing it measured C5 -0.3 %, C4 +2.8 %)
                 using XS = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, 0>;
-                if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XS>(p, v, ring + scene, stream);
-                else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XS>(p, v, ring, stream);
+                if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XS>(p, vw, ring + scene, stream);
+                else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XS>(p, vw, ring, stream);
                 return;
             }
             if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES>(p, v, ring + scene, stream);
