@@ -621,6 +621,18 @@ struct Rec {  // HitRecord (hitable.rs:14-22) of the closest hit, world space
     bool front;
     uint32_t mat;
 };
+// World-mode sphere records leave u = UV_DEFERRED (no hit has it: u is in [0, 1]) and sphere_uv
+// computes (u, v) when a texture needs them (HitRecord::new_with_uv's sphere uv, sphere.rs:148-161):
+// the outward normal is n on the front face, -n on the back (n = -signum(d . outward) * outward).
+constexpr float UV_DEFERRED = -2.0f;
+template <typename R>
+__device__ __forceinline__ void sphere_uv(const Rec<R>& h, R& u, R& v) {
+    const V<R> geo = h.front ? h.n : -h.n;
+    const R theta = acos(-geo.y);
+    const R phi = atan2(-geo.z, geo.x) + R(M_PI);
+    u = phi * R(1.0 / (2.0 * M_PI));
+    v = theta * R(1.0 / M_PI);
+}
 
 // hit point / normal back out (inner -> outer); Scale leaves the normal alone (scale.rs:82-85)
 template <typename R>
@@ -1899,10 +1911,10 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
         // would leave the next ray's origin off the surface by more than the t_min of 0.001 hides)
         if (NRT_SPHERE_REPROJ && sizeof(R) == 4 && q.AB[6] == R(0)) h.p = center + fabs(q.D) * geo;
         shade = geo;
-        const R theta = acos(-geo.y);
-        const R phi = atan2(-geo.z, geo.x) + R(M_PI);
-        h.u = phi * R(1.0 / (2.0 * M_PI));
-        h.v = theta * R(1.0 / M_PI);
+        // uv (acos / atan2) only where a texture reads it: sphere_uv, from the record's normal
+        // (the ground sphere of the earth scene is solid: 18 % of its shading was this record)
+        h.u = R(UV_DEFERRED);
+        h.v = R(0);
     } else {
         h.u = dot(h.p, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
         h.v = dot(h.p, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
@@ -2223,6 +2235,12 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // writes, but the extra round trip before each fetch cost C3 earth 6.67 -> 7.32 ms): off
 #define NRT_PROBE_HEAD 0
 #endif
+#ifndef NRT_DUAL
+#define NRT_DUAL 0  // world-BVH Philox loop: a second path context per lane (A/B via NRT_JIT_DEFS)
+#endif
+#ifndef NRT_DUAL_SWAP
+#define NRT_DUAL_SWAP 8u  // DUAL: lanes ready to swap contexts before a swap round
+#endif
 #ifndef NRT_FETCH_AHEAD
 #define NRT_FETCH_AHEAD 64u  // Philox: take the next group when fewer samples are left to claim
 #endif
@@ -2346,8 +2364,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     uint4 w = make_uint4(0u, 0u, 0u, 0u);  // Philox: this segment's block
 
     auto albedo = [&](const MatV<R>& m, const Rec<R>& h) {
-        if constexpr (FLAT) return m.color;  // every texture is a SolidColor
-        else return m.solid ? m.color : tex_color<R, PERLIN>(sc, m.tex, h.u, h.v, h.p);
+        if constexpr (FLAT) {
+            return m.color;  // every texture is a SolidColor
+        } else {
+            if (m.solid) return m.color;
+            R u = h.u, v = h.v;
+            if (MAXD <= 0 && u == R(UV_DEFERRED)) sphere_uv(h, u, v);
+            return tex_color<R, PERLIN>(sc, m.tex, u, v, h.p);
+        }
     };
 
     auto material = [&](uint32_t mat) {  // the material table is LDS-resident: re-reading is cheap
@@ -2783,6 +2807,36 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         };
         const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
 
+        // NRT_DUAL (world-BVH mode): each lane holds a second path context S beside the working
+        // one W (the registers above).  W is the one traversed; S is parked: READY (its next ray
+        // waits for traversal) or WAIT (traversed, its hit waits for shading).  A lane whose
+        // traversal ends while S is READY swaps the two and traverses on (swap rounds, cheap)
+        // instead of idling until the wave's shading round; a shading round shades one waiting
+        // context per lane (S swapped into the working registers and back) or gives an empty
+        // context a new sample.  Sample values do not depend on which lane or context ran them.
+        constexpr bool DUAL = MAXD < 0 && NRT_DUAL && !PROF;
+        constexpr uint32_t S_READY = 1u, S_WAIT = 2u;
+        Ray<R> s_ray = ray;
+        V<R> s_tp = tp;
+        uint32_t s_b = 0, s_slot = 0, s_j = 0, s_cur = 0, s_pxy = 0, s_phase = 0;
+        bool s_alive = false, s_killed = false, s_bounced = false;
+        float s_t = INFINITY;
+        int32_t s_prim = -1;
+        auto swap_ctx = [&]() {
+            const Ray<R> r0 = ray; ray = s_ray; s_ray = r0;
+            const V<R> t0v = tp; tp = s_tp; s_tp = t0v;
+            uint32_t u;
+            u = b; b = s_b; s_b = u;
+            u = slot; slot = s_slot; s_slot = u;
+            u = j; j = s_j; s_j = u;
+            u = cur; cur = s_cur; s_cur = u;
+            u = pxy; pxy = s_pxy; s_pxy = u;
+            bool f;
+            f = alive; alive = s_alive; s_alive = f;
+            f = killed; killed = s_killed; s_killed = f;
+            f = bounced; bounced = s_bounced; s_bounced = f;
+        };
+
         while (true) {
             // Group bookkeeping at the loop head, where little state is live: write out
             // finished groups, and take the next group into the free slot as soon as
@@ -2803,20 +2857,45 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 for (uint32_t k = 0; k < NS; ++k) free |= k == r && gids[k] == NO_GROUP;
                 if (free) fetch(r);
             }
-            if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
+            if (exhausted && !ready && GS - next == 0u && __ballot(alive || (DUAL && s_alive)) == 0ull) break;
             const unsigned long long t0 = stamp();
             HitMin<R, MAXD> hm;
             bool hit = false, sh, traced;
+            bool tgt_s = false;  // DUAL: the spare context is in the working registers this round
             if constexpr (MAXD < 0) {
                 // World-BVH mode: lanes keep their traversal state across rounds; the wave
                 // traverses until a ballot shows >= p.wave_wait lanes finished, then only
                 // those lanes shade (active-ray compaction within the wave).
                 static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
-                while (true) {
-                    const bool going = alive && ts.busy();
-                    if (__ballot(going) == 0ull) break;
-                    if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
-                    if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
+                if constexpr (DUAL) {
+                    while (true) {
+                        const bool going = alive && ts.busy();
+                        const bool fin = alive && !ts.busy();
+                        const bool sready = s_alive && s_phase == S_READY;
+                        const uint64_t gm = __ballot(going), swm = __ballot(fin && sready);
+                        const uint32_t nstall = (uint32_t)__popcll(__ballot(fin && !sready));
+                        if (nstall >= wait_min || (gm == 0ull && swm == 0ull)) break;  // shading round
+                        if (swm != 0ull && ((uint32_t)__popcll(swm) >= NRT_DUAL_SWAP || gm == 0ull)) {
+                            if (fin && sready) {  // park W's hit in S, traverse S's ray
+                                const float t_hit = ts.t_best;
+                                const int32_t p_hit = ts.best;
+                                swap_ctx();
+                                s_phase = S_WAIT;
+                                s_t = t_hit;
+                                s_prim = p_hit;
+                                begin();
+                            }
+                            continue;
+                        }
+                        if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, nullptr);
+                    }
+                } else {
+                    while (true) {
+                        const bool going = alive && ts.busy();
+                        if (__ballot(going) == 0ull) break;
+                        if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
+                        if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
+                    }
                 }
                 sh = alive && !ts.busy();
                 if constexpr (PROF) {
@@ -2827,6 +2906,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 hm.prim = (uint32_t)ts.best;
                 hm.depth = 0;
                 hit = ts.best >= 0;
+                if constexpr (DUAL) {
+                    // this round's target per lane: W if it waits; else S if it waits, or S if it
+                    // is empty while W traverses (a new sample for it); else nothing (or W's claim)
+                    const bool w_wait = alive && !ts.busy();
+                    tgt_s = !w_wait && ((s_alive && s_phase == S_WAIT) || (!s_alive && alive));
+                    if (tgt_s) {
+                        swap_ctx();
+                        sh = alive;  // S waited (or is empty: alive false, it only claims)
+                        traced = sh && !killed && b < p.max_bounces;
+                        hm.t = s_t;
+                        hm.prim = (uint32_t)s_prim;
+                        hit = s_prim >= 0;
+                    }
+                }
             } else {
                 sh = alive;
                 traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
@@ -2896,7 +2989,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 camera();
                 killed = pxy == PAD_XY;  // padding sample: no pixel, ends at once
             }
-            if ((sh || want) && alive) begin();
+            if constexpr (DUAL) {
+                if (tgt_s) {  // S's new segment (or sample) is ready; W's traversal goes on
+                    swap_ctx();
+                    s_phase = S_READY;
+                } else if ((sh || want) && alive) {
+                    begin();
+                }
+                if (!alive && s_alive && s_phase == S_READY) {  // W is empty: traverse S's ray
+                    swap_ctx();
+                    begin();
+                }
+            } else if ((sh || want) && alive) {
+                begin();
+            }
             if constexpr (PROF) {
                 const unsigned long long t4 = stamp();
                 const uint32_t busy = (uint32_t)__popcll(__ballot(sh));

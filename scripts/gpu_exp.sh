@@ -9,7 +9,7 @@ C4="--scene scenes/utah-teapot-scene.json"; C3="--scene scenes/earth.toml --widt
 C5X="--precision f64 --rng chacha8 --spp 64"; C4X="$C4 --precision f64 --rng chacha8 --spp 16"
 AB="timeout -k 10 900 python scripts/ab_configs.py --reps 2"
 BASE=nr-ray-tracer_amd/ab/base/libnrt.so; NEW=nr-ray-tracer_amd/nrt/libnrt.so
-$AB --out gpurun_out/${tag}_x.jsonl --lib new=$NEW --lib ifif=nr-ray-tracer_amd/ab/ifif/libnrt.so --lib lw4=nr-ray-tracer_amd/ab/lw4/libnrt.so --cfg c5x="$C5X" --cfg c4x="$C4X" || exit 1
+$AB --out gpurun_out/${tag}_c3.jsonl --lib prev=nr-ray-tracer_amd/ab/prev/libnrt.so --lib new=$NEW --cfg c3="$C3" --cfg c3c="$C3 --rng chacha8 --spp 16" || exit 1
 pmc() {  # name lib counters bench-args...
   local n=$1 lib=$2 c=$3; shift 3
   env NRT_LIB=$PWD/$lib timeout -s KILL 180 rocprofv3 --pmc $c -d gpurun_out/${tag}_pmc_$n -o run --output-format csv -- python3 bench.py --no-cpu-baseline --kernel-only --steps 2 --warmup 1 "$@" > /dev/null 2> gpurun_out/${tag}_pmc_$n.err || { echo "pmc $n failed"; tail -3 gpurun_out/${tag}_pmc_$n.err; exit 1; }
