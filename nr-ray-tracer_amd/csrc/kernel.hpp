@@ -2235,12 +2235,6 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 // writes, but the extra round trip before each fetch cost C3 earth 6.67 -> 7.32 ms): off
 #define NRT_PROBE_HEAD 0
 #endif
-#ifndef NRT_DUAL
-#define NRT_DUAL 0  // world-BVH Philox loop: a second path context per lane (A/B via NRT_JIT_DEFS)
-#endif
-#ifndef NRT_DUAL_SWAP
-#define NRT_DUAL_SWAP 8u  // DUAL: lanes ready to swap contexts before a swap round
-#endif
 #ifndef NRT_FETCH_AHEAD
 #define NRT_FETCH_AHEAD 64u  // Philox: take the next group when fewer samples are left to claim
 #endif
@@ -2807,36 +2801,6 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         };
         const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
 
-        // NRT_DUAL (world-BVH mode): each lane holds a second path context S beside the working
-        // one W (the registers above).  W is the one traversed; S is parked: READY (its next ray
-        // waits for traversal) or WAIT (traversed, its hit waits for shading).  A lane whose
-        // traversal ends while S is READY swaps the two and traverses on (swap rounds, cheap)
-        // instead of idling until the wave's shading round; a shading round shades one waiting
-        // context per lane (S swapped into the working registers and back) or gives an empty
-        // context a new sample.  Sample values do not depend on which lane or context ran them.
-        constexpr bool DUAL = MAXD < 0 && NRT_DUAL && !PROF;
-        constexpr uint32_t S_READY = 1u, S_WAIT = 2u;
-        Ray<R> s_ray = ray;
-        V<R> s_tp = tp;
-        uint32_t s_b = 0, s_slot = 0, s_j = 0, s_cur = 0, s_pxy = 0, s_phase = 0;
-        bool s_alive = false, s_killed = false, s_bounced = false;
-        float s_t = INFINITY;
-        int32_t s_prim = -1;
-        auto swap_ctx = [&]() {
-            const Ray<R> r0 = ray; ray = s_ray; s_ray = r0;
-            const V<R> t0v = tp; tp = s_tp; s_tp = t0v;
-            uint32_t u;
-            u = b; b = s_b; s_b = u;
-            u = slot; slot = s_slot; s_slot = u;
-            u = j; j = s_j; s_j = u;
-            u = cur; cur = s_cur; s_cur = u;
-            u = pxy; pxy = s_pxy; s_pxy = u;
-            bool f;
-            f = alive; alive = s_alive; s_alive = f;
-            f = killed; killed = s_killed; s_killed = f;
-            f = bounced; bounced = s_bounced; s_bounced = f;
-        };
-
         while (true) {
             // Group bookkeeping at the loop head, where little state is live: write out
             // finished groups, and take the next group into the free slot as soon as
@@ -2857,45 +2821,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 for (uint32_t k = 0; k < NS; ++k) free |= k == r && gids[k] == NO_GROUP;
                 if (free) fetch(r);
             }
-            if (exhausted && !ready && GS - next == 0u && __ballot(alive || (DUAL && s_alive)) == 0ull) break;
+            if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
             const unsigned long long t0 = stamp();
             HitMin<R, MAXD> hm;
             bool hit = false, sh, traced;
-            bool tgt_s = false;  // DUAL: the spare context is in the working registers this round
             if constexpr (MAXD < 0) {
                 // World-BVH mode: lanes keep their traversal state across rounds; the wave
                 // traverses until a ballot shows >= p.wave_wait lanes finished, then only
                 // those lanes shade (active-ray compaction within the wave).
                 static_assert(sizeof(R) == 4, "world-BVH mode is an f32-kernel mode");
-                if constexpr (DUAL) {
-                    while (true) {
-                        const bool going = alive && ts.busy();
-                        const bool fin = alive && !ts.busy();
-                        const bool sready = s_alive && s_phase == S_READY;
-                        const uint64_t gm = __ballot(going), swm = __ballot(fin && sready);
-                        const uint32_t nstall = (uint32_t)__popcll(__ballot(fin && !sready));
-                        if (nstall >= wait_min || (gm == 0ull && swm == 0ull)) break;  // shading round
-                        if (swm != 0ull && ((uint32_t)__popcll(swm) >= NRT_DUAL_SWAP || gm == 0ull)) {
-                            if (fin && sready) {  // park W's hit in S, traverse S's ray
-                                const float t_hit = ts.t_best;
-                                const int32_t p_hit = ts.best;
-                                swap_ctx();
-                                s_phase = S_WAIT;
-                                s_t = t_hit;
-                                s_prim = p_hit;
-                                begin();
-                            }
-                            continue;
-                        }
-                        if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, nullptr);
-                    }
-                } else {
-                    while (true) {
-                        const bool going = alive && ts.busy();
-                        if (__ballot(going) == 0ull) break;
-                        if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
-                        if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
-                    }
+                while (true) {
+                    const bool going = alive && ts.busy();
+                    if (__ballot(going) == 0ull) break;
+                    if ((uint32_t)__popcll(__ballot(alive && !ts.busy())) >= wait_min) break;
+                    if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack, PROF ? prof[wave] : nullptr);
                 }
                 sh = alive && !ts.busy();
                 if constexpr (PROF) {
@@ -2906,20 +2845,6 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 hm.prim = (uint32_t)ts.best;
                 hm.depth = 0;
                 hit = ts.best >= 0;
-                if constexpr (DUAL) {
-                    // this round's target per lane: W if it waits; else S if it waits, or S if it
-                    // is empty while W traverses (a new sample for it); else nothing (or W's claim)
-                    const bool w_wait = alive && !ts.busy();
-                    tgt_s = !w_wait && ((s_alive && s_phase == S_WAIT) || (!s_alive && alive));
-                    if (tgt_s) {
-                        swap_ctx();
-                        sh = alive;  // S waited (or is empty: alive false, it only claims)
-                        traced = sh && !killed && b < p.max_bounces;
-                        hm.t = s_t;
-                        hm.prim = (uint32_t)s_prim;
-                        hit = s_prim >= 0;
-                    }
-                }
             } else {
                 sh = alive;
                 traced = alive && !killed && b < p.max_bounces;  // depth cap returns black (Q6)
@@ -2989,20 +2914,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 camera();
                 killed = pxy == PAD_XY;  // padding sample: no pixel, ends at once
             }
-            if constexpr (DUAL) {
-                if (tgt_s) {  // S's new segment (or sample) is ready; W's traversal goes on
-                    swap_ctx();
-                    s_phase = S_READY;
-                } else if ((sh || want) && alive) {
-                    begin();
-                }
-                if (!alive && s_alive && s_phase == S_READY) {  // W is empty: traverse S's ray
-                    swap_ctx();
-                    begin();
-                }
-            } else if ((sh || want) && alive) {
-                begin();
-            }
+            if ((sh || want) && alive) begin();
             if constexpr (PROF) {
                 const unsigned long long t4 = stamp();
                 const uint32_t busy = (uint32_t)__popcll(__ballot(sh));
