@@ -234,6 +234,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        # every rank runs the scene-specialised kernel or none renders: a rank on the generic kernel
+        # (FMA contraction can part at the ulp level) would make the frame differ from N = 1's
+        os.environ.setdefault("NRT_JIT", "require")
     if world != args.gpus and world == 1:
         raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     ndev = torch.cuda.device_count()

@@ -147,7 +147,8 @@ int nrt_abi_version(void);
  * counterpart) */
 const char* nrt_build_id(void);
 /* Scene-specialised kernels (built with hiprtc, loaded lazily, when a scene is first rendered
- * in an f32 world mode; NRT_JIT=0 turns them off).  The first such render of a scene in a
+ * in an f32 world mode; NRT_JIT=0 turns them off, NRT_JIT=require makes a failed build an
+ * error of the render call instead of a fallback to the generic kernel).  The first such render of a scene in a
  * process pays the compile (~1 s) inside the render call.  out[0] = kernels built in this
  * process, out[1] = renders that used one, out[2] = builds that failed (the generic kernel
  * rendered instead: slower, and its f32 frames may differ in the last bits), out[3] = compile

@@ -45,7 +45,7 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
         const uint32_t npix = p0.pixel_end - p0.pixel_begin;
         const uint32_t lds = lds_fixed + dev::RING * dev::BLOCK * (uint32_t)sizeof(uint2) + stack;
         const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
-        launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(need, resident(lds))), lds, p0);
+        launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({need, resident(lds), chacha_grid_cap()})), lds, p0);
         return;
     }
     if (maxd == MODE_WORLD_BVH)  // below the staged scene: the traversal stack (launch_one's ring)

@@ -39,6 +39,8 @@ struct JitStats {
     uint64_t compile_ns = 0;  // wall time spent in hiprtc + module load
 };
 void* jit_render_kernel(const std::string& targs, int device);
+// throws under NRT_JIT=require (jit.hip): called when jit_render_kernel returned null
+void jit_require_failed(const std::string& targs);
 JitStats jit_stats();
 uint64_t jit_compile_only(const std::string& targs, std::string* log);  // code bytes, 0 on failure (tests)
 // stack_entry: bytes per world-BVH stack entry (2 for the compact tree, kernel.hpp StackEntry)

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "kernel.hpp"
@@ -9,6 +10,14 @@
 
 namespace nrt {
 
+
+// ChaCha8 persistent lanes: a cap on the grid (knob NRT_CHACHA_GRID, tests: a small grid hands out
+// most pixels through the per-XCD counters; the frame must not change).
+inline uint64_t chacha_grid_cap() {
+    const char* e = std::getenv("NRT_CHACHA_GRID");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return v > 0 ? (uint64_t)v : ~0ull;
+}
 
 // Blocks the device keeps resident for one kernel variant.
 template <typename K>
@@ -65,7 +74,7 @@ static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint3
     const uint32_t npix = p0.pixel_end - p0.pixel_begin;
     if constexpr (G::exact_stream) {  // persistent lanes (render_kernel): the resident workgroups at most
         const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
-        const uint64_t blocks = std::max<uint64_t>(1, std::min(need, resident_blocks(kernel, lds_fixed)));
+        const uint64_t blocks = std::max<uint64_t>(1, std::min({need, resident_blocks(kernel, lds_fixed), chacha_grid_cap()}));
         hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
     } else {
         philox_launch<MAXD>(

@@ -287,7 +287,9 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
                 if (rng == RNG_PHILOX && !ds->wruns.empty() && ds->wruns.size() <= JIT_MAX_RUNS) {
                     targs += "nrt::dev::WorldSig<";
                     for (size_t i = 0; i < ds->wruns.size(); ++i) targs += (i ? ", " : "") + std::to_string(ds->wruns[i]) + "u";
-                    jit = jit_render_kernel(targs + ">", ds->device);
+                    targs += ">";
+                    jit = jit_render_kernel(targs, ds->device);
+                    if (!jit) jit_require_failed(targs);
                 }
             } else if (ds->flat) {  // (if-if trips: teapot 41.1 -> 40.5 ms; the sphere rounds measured slower)
                 // the compact 4-wide tree where the scene has one (knob NRT_WBVH_COMPACT=0: the 64-byte one)
@@ -297,6 +299,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
                 targs += std::string("nrt::dev::BvhSig<") + (compact ? "5, " : v.wbvh4 ? "4, " : "2, ") +
                          ((v.wflags & WFLAG_COPLANAR) ? "true, " : "false, ") + std::to_string(ds->wbvh_kinds) + ">";
                 jit = jit_render_kernel(targs, ds->device);
+                if (!jit) jit_require_failed(targs);
             }
         }
         if (jit) launch_fast_jit(q, v, jit, lds_fixed, maxd, rng, jit ? stack_entry : 4u, stream);

@@ -318,6 +318,45 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), name
 
 
+@pytest.mark.parametrize("scene,w,h,spp,precision", [
+    ("scenes/cornell-box-scene.json", 48, 40, 4, "f64"),
+    ("scenes/utah-teapot-scene.json", 40, 32, 2, "f64"),
+    ("scenes/earth.toml", 64, 36, 2, "f64"),
+    ("scenes/cornell-box-scene.json", 48, 40, 4, "f32"),
+    ("scenes/utah-teapot-scene.json", 40, 32, 2, "f32"),
+])
+def test_chacha8_persistent_lanes_grid_invariant(scene, w, h, spp, precision, monkeypatch):
+    """ChaCha8 kernels run persistent lanes (kernel.hpp, exact_stream branch): a lane renders pixel
+    after pixel, each with its own stream and its samples in order (camera.rs:318-331), the pixels
+    past the grid's first round handed out by per-XCD counters.  A pixel's value depends on its
+    index alone, so the frame is the same bit for bit whatever the grid: one or three workgroups
+    (NRT_CHACHA_GRID) send nearly every pixel through the counters and their steal path."""
+    s = load(scene, w, h, spp)
+    base = s.render(precision=precision, rng="chacha8")
+    assert np.isfinite(base).all() and base.max() > 0
+    for grid in ("1", "3"):
+        monkeypatch.setenv("NRT_CHACHA_GRID", grid)
+        img = s.render(precision=precision, rng="chacha8")
+        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), grid
+
+
+def test_jit_require_refuses_the_generic_fallback(monkeypatch):
+    """NRT_JIT=require (jit.hip; bench.py sets it for N > 1): a scene-specialised build that fails
+    is an error of the render call, not a silent fallback to the generic kernel, whose f32 frame
+    can part from the specialised one's in the last bits; without it the generic kernel renders
+    and nrt_jit_stats counts the failure."""
+    s = load("scenes/cornell-box-scene.json", 32, 24, 2)
+    monkeypatch.setenv("NRT_JIT_DEFS", "-DNRT_GRAB=not_a_number")  # a build that cannot compile
+    monkeypatch.setenv("NRT_JIT", "require")
+    with pytest.raises(nrt.NrtError, match="NRT_JIT=require"):
+        s.render(precision="f32", rng="philox", trace="world-list")
+    monkeypatch.setenv("NRT_JIT", "1")
+    before = nrt.jit_stats()
+    img = s.render(precision="f32", rng="philox", trace="world-list")
+    assert np.isfinite(img).all() and img.max() > 0
+    assert nrt.jit_stats()["launches"] == before["launches"]  # the generic kernel rendered
+
+
 def test_exact_world_mode_far_camera(monkeypatch):
     """The exact world mode culls with f32 boxes padded by 1e-6 of the scene's extent, enough for
     ray origins within ~7x that extent; a camera farther out makes make_params (api.cpp) take the
