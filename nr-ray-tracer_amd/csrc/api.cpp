@@ -211,7 +211,9 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
         for (int q = 0; q < 7; ++q) p.camf[q][k] = (float)vs[q][k];
         if (c.defocus_disk_u[k] != 0.0 || c.defocus_disk_v[k] != 0.0) p.defocus = 1;
     }
-    p.wave_wait = 32;  // world-BVH shading-round threshold (C4 +4 %, C1 +13 % over 8; tuning knob NRT_WAVE_WAIT, 1..64)
+    // world-BVH shading-round threshold (C4 +4 %, C1 +13 % over 8); 0 = chosen per kernel variant
+    // in gpu_launch_render (32 for the speculative rounds, 24 for the if-if trips); knob NRT_WAVE_WAIT 1..64
+    p.wave_wait = 0;
     if (const char* e = std::getenv("NRT_WAVE_WAIT")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) p.wave_wait = (uint32_t)v;
@@ -249,6 +251,8 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // (C5 f64 54.9 / 55.0 ms, C4 15.2 / 14.7 ms); knob NRT_EXACT_LSTACK=0 for the scratch stack
     p.exact_lstack = 1;
     if (const char* e = std::getenv("NRT_EXACT_LSTACK")) p.exact_lstack = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+    p.exact_slots = 0;  // knob NRT_EXACT_SLOTS=1: small scenes' prefilter over every slot, no walk
+    if (const char* e = std::getenv("NRT_EXACT_SLOTS")) p.exact_slots = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;

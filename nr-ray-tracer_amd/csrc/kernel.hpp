@@ -37,8 +37,8 @@ constexpr int BLOCK = 256;
 #ifndef NRT_WBVH_SORT
 #define NRT_WBVH_SORT 0  // 4-wide visits: 1 = full sorting network; 0 = nearest hit child first, the rest in slot order (C4 +4 %)
 #endif
-#ifndef NRT_LEAF_PER_TRIP
-#define NRT_LEAF_PER_TRIP 1  // if-if trips: primitives of a leaf one lane tests per trip
+#ifndef NRT_WBVH_UNIFIED
+#define NRT_WBVH_UNIFIED 1  // if-if trips: a visit and a primitive test in the same trip (C4 40.2 -> 34.6 ms)
 #endif
 #ifndef NRT_WBVH_IFIF
 // world BVH: one node visit or one primitive per lane and trip (wbvh_trip) in the KF_FLAT
@@ -889,7 +889,7 @@ struct WorldSig {
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
 // the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
 // plane-only scenes, and the unfiltered walk it falls back to).
-enum : int { EXACT_SIG_WORLD_PF = 1 };
+enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2 };
 template <int MODE, int WIDTH, bool LSTACK = false>
 struct ExactSig {
     static constexpr uint32_t n = 0;
@@ -1334,20 +1334,20 @@ __device__ __forceinline__ void wbvh_round_impl(WbvhTrav& ts, const DSceneView<R
 template <typename R, int W, bool FLAT, bool TIE, int PRIMS = 0, class STKP>
 __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray,
                                                STKP stack, unsigned long long* pc) {
-    if (ts.leaf != WBVH_NO_LEAF) {
+    const bool leaf_now = ts.leaf != WBVH_NO_LEAF;
+    if (leaf_now) {  // (two primitives per trip measured C4 -6 %, round 2; 41.6 ms against 40.2, round 3)
         prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
-#pragma unroll
-        for (int u = 0; u < NRT_LEAF_PER_TRIP; ++u) {  // up to NRT_LEAF_PER_TRIP primitives of the leaf
-            if (u > 0 && ts.leaf == WBVH_NO_LEAF) break;
-            const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
-            const DPrimWorld<float> q = load16(sc.wprims + first);
-            const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
-            const bool ok = t >= 0.0f;
-            ts.t_best = ok ? t : ts.t_best;
-            ts.best = ok ? (int32_t)first : ts.best;
-            ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
-        }
-    } else if (ts.node >= 0) {
+        const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
+        const DPrimWorld<float> q = load16(sc.wprims + first);
+        const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
+        const bool ok = t >= 0.0f;
+        ts.t_best = ok ? t : ts.t_best;
+        ts.best = ok ? (int32_t)first : ts.best;
+        ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+    }
+    // NRT_WBVH_UNIFIED: a lane holding both a leaf cursor and a node does both in one trip (a trip
+    // runs both branches whenever the wave's lanes are mixed anyway); otherwise one or the other
+    if ((NRT_WBVH_UNIFIED || !leaf_now) && ts.node >= 0) {
         prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
         wbvh_visit_w<W>(ts, sc, stack);
     }
@@ -1815,14 +1815,16 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
         wbvh_begin(ts, wbvh_root(sc), fr);
         auto walk = [&](auto& stk) {
 #if NRT_EXACT_IFIF
-            // if-if trips: one node visit or one primitive offer per lane per trip
+            // if-if trips: one primitive offer and (2: also) one node visit per lane per trip
             int32_t leaf = WBVH_NO_LEAF;  // leaf cursor ~(first << 3 | more)
             while (true) {
-                if (leaf != WBVH_NO_LEAF) {
+                const bool leaf_now = leaf != WBVH_NO_LEAF;
+                if (leaf_now) {
                     const uint32_t v = ~(uint32_t)leaf, first = v >> 3, more = v & 7u;
                     if (c.offer(load16(sc.wxprims + first), fr, first)) ts.t_best = c.bound * (1.0f + 0x1p-20f);
                     leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
-                } else if (ts.node >= 0) {
+                }
+                if ((NRT_EXACT_IFIF == 2 || !leaf_now) && ts.node >= 0) {
                     wbvh4c_visit<R>(ts, sc, stk);
                 }
                 if (leaf == WBVH_NO_LEAF && ts.node < 0) {
@@ -1864,13 +1866,71 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     return xcands_finish(c, sc, wray, hm);
 }
 
+// Small plane-only scenes (at most EXACT_SLOTS_MAX slots, EXACT_SIG_SLOTS_PF): the prefilter over
+// every slot of the culling tree in slot order instead of the walk: the slot index is wave-
+// uniform, so each f32 record arrives by scalar load and no lane waits for another's walk (no
+// stack, no divergence).  Slot order instead of walk order changes neither the candidate set's
+// outcome nor the winner (smallest exact t, ties to the higher rank: xcands_finish).  More than
+// XCAND live candidates (never seen on the reference scenes): the reference tests on every slot.
+constexpr uint32_t EXACT_SLOTS_MAX = 32;
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_exact_slots_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    static_assert(sizeof(R) == 8, "exact world mode is an f64-kernel mode");
+    Ray<float> fr;
+    fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    XCands c;
+    c.init();
+    const ConstU32 wq = (ConstU32)sc.wxprims;
+    const uint32_t n = sc.n_wexact;
+    constexpr uint32_t QW = (uint32_t)(sizeof(DPrimWorld<float>) / 4);
+    for (uint32_t k = 0; k < n; ++k) {
+        uint32_t w[QW];
+#pragma unroll
+        for (uint32_t i = 0; i < QW; ++i) w[i] = wq[k * QW + i];  // (s_load: k is wave-uniform)
+        DPrimWorld<float> q;
+        __builtin_memcpy(&q, w, sizeof q);
+        c.offer(q, fr, k);
+    }
+    if (!c.over) return xcands_finish(c, sc, wray, hm);
+    R best_t = R(INFINITY);  // overflow: the reference tests on every slot (at most EXACT_SLOTS_MAX)
+    uint32_t best_rank = 0;
+    int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
+    Ray<R> oray = wray;
+    for (uint32_t k = 0; k < n; ++k) {
+        const DExactRef ref = sc.wexact[k];
+        if (ref.inst != cur_inst) {
+            oray = wray;
+            if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
+            cur_inst = ref.inst;
+        }
+        R alpha, beta;
+        V<R> point;
+        const R t = plane_t(sc.prims[ref.prim], oray, alpha, beta, point);
+        if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
+            best_t = t;
+            best_rank = ref.rank;
+            best_prim = (int32_t)ref.prim;
+            best_inst = ref.inst;
+        }
+    }
+    hm.t = best_t;
+    hm.prim = (uint32_t)best_prim;
+    hm.depth = best_inst >= 0 ? 1 : 0;
+    hm.inst[0] = (uint32_t)best_inst;
+    return best_prim >= 0;
+}
+
 template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       STKP stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0,
                                       bool xthread = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
-    else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
+    else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_SLOTS_PF) {
+        static_assert(PF, "EXACT_SIG_SLOTS_PF is a KF_PLANES variant");
+        return trace_exact_slots_pf<R, MAXD>(sc, wray, hm);
+    } else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
         static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
         if constexpr (SIG::lstack) return trace_exact_wbvh_pf<R, MAXD, SIG::bvh, true>(sc, wray, hm, false, stack);
         else return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);

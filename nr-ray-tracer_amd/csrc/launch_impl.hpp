@@ -124,6 +124,12 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                     else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XT>(p, vw, ring, stream);
                     return;
                 }
+                if (p.exact_slots && vw.n_wexact <= dev::EXACT_SLOTS_MAX) {  // small scenes: every slot, no walk
+                    using XA = dev::ExactSig<dev::EXACT_SIG_SLOTS_PF, 0>;
+                    if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XA>(p, vw, ring + scene, stream);
+                    else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XA>(p, vw, ring, stream);
+                    return;
+                }
                 if (vw.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
                     using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
                     const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);

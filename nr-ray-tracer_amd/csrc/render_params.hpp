@@ -77,6 +77,9 @@ struct RenderParams {
     // Exact world mode on the compact tree: its traversal stack in LDS (16-bit entries) and
     // 3 waves per SIMD (default), or a private (scratch) stack at 4 (ExactSig lstack).
     uint32_t exact_lstack;
+    // Exact world mode with the prefilter, at most EXACT_SLOTS_MAX slots: the prefilter over every
+    // slot in order (scalar loads, no walk) instead of the culling walk (EXACT_SIG_SLOTS_PF).
+    uint32_t exact_slots;
     float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
 };
 

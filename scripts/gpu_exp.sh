@@ -9,7 +9,8 @@ C4="--scene scenes/utah-teapot-scene.json"; C3="--scene scenes/earth.toml --widt
 C5X="--precision f64 --rng chacha8 --spp 64"; C4X="$C4 --precision f64 --rng chacha8 --spp 16"
 AB="timeout -k 10 900 python scripts/ab_configs.py --reps 2"
 BASE=nr-ray-tracer_amd/ab/base/libnrt.so; NEW=nr-ray-tracer_amd/nrt/libnrt.so
-$AB --out gpurun_out/${tag}_all.jsonl --lib prev=nr-ray-tracer_amd/ab/prev/libnrt.so --lib new=$NEW --cfg c5="" --cfg c4="$C4" --cfg c3="$C3" --cfg c5x="$C5X" || exit 1
+$AB --out gpurun_out/${tag}_c4.jsonl --lib new=$NEW --env ww16="NRT_WAVE_WAIT=16" --env ww20="NRT_WAVE_WAIT=20" --env ww24="NRT_WAVE_WAIT=24" --env ww28="NRT_WAVE_WAIT=28" --env ww32="" --cfg c4="$C4" --cfg c1b="$C1B" || exit 1
+$AB --out gpurun_out/${tag}_x.jsonl --lib new=$NEW --lib uni=nr-ray-tracer_amd/ab/uni/libnrt.so --cfg c5x="$C5X" --cfg c4x="$C4X" || exit 1
 pmc() {  # name lib counters bench-args...
   local n=$1 lib=$2 c=$3; shift 3
   env NRT_LIB=$PWD/$lib timeout -s KILL 180 rocprofv3 --pmc $c -d gpurun_out/${tag}_pmc_$n -o run --output-format csv -- python3 bench.py --no-cpu-baseline --kernel-only --steps 2 --warmup 1 "$@" > /dev/null 2> gpurun_out/${tag}_pmc_$n.err || { echo "pmc $n failed"; tail -3 gpurun_out/${tag}_pmc_$n.err; exit 1; }

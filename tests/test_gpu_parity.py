@@ -296,10 +296,12 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     frames are equal bit for bit (BVH::hit, object.rs:89-121)."""
     s = load(scene, w, h, spp)
     frames = {}
-    # (all, world, prefilter, LDS stack): the world walks run on the compact tree (16-bit stack
-    # entries, in scratch or, with NRT_EXACT_LSTACK, in LDS at 3 waves per SIMD)
-    modes = {"bvh": ("0", "0", "0", "0"), "all": ("1", "0", "0", "0"), "world": ("0", "1", "0", "0"),
-             "world_pf": ("0", "1", "1", "0"), "world_pf_lds_stack": ("0", "1", "1", "1")}
+    # (all, world, prefilter, LDS stack, slots): the world walks run on the compact tree (16-bit stack
+    # entries, in scratch or, with NRT_EXACT_LSTACK, in LDS at 3 waves per SIMD); small plane-only
+    # scenes can prefilter every slot in order instead of walking (NRT_EXACT_SLOTS)
+    modes = {"bvh": ("0", "0", "0", "0", "0"), "all": ("1", "0", "0", "0", "0"), "world": ("0", "1", "0", "0", "0"),
+             "world_pf": ("0", "1", "1", "0", "0"), "world_pf_lds_stack": ("0", "1", "1", "1", "0"),
+             "world_pf_slots": ("0", "1", "1", "1", "1")}
     for name, env in modes.items():
         if name.startswith("world") and s.stats()["exact_mode"] != 2:
             continue
@@ -307,10 +309,12 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
         monkeypatch.setenv("NRT_EXACT_WBVH", env[1])
         monkeypatch.setenv("NRT_EXACT_PF", env[2])
         monkeypatch.setenv("NRT_EXACT_LSTACK", env[3])
+        monkeypatch.setenv("NRT_EXACT_SLOTS", env[4])
         frames[name] = s.render(precision="f64", rng="chacha8")
     if s.stats()["exact_mode"] == 2:  # the 4-wide tree with 32-bit refs (NRT_EXACT_COMPACT=0, read at upload)
         monkeypatch.setenv("NRT_EXACT_COMPACT", "0")
         monkeypatch.setenv("NRT_EXACT_LSTACK", "0")
+        monkeypatch.setenv("NRT_EXACT_SLOTS", "0")
         frames["world_pf_wide"] = load(scene, w, h, spp).render(precision="f64", rng="chacha8")
     base = frames.pop("bvh")
     assert np.isfinite(base).all()
