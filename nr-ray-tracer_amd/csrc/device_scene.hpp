@@ -116,8 +116,8 @@ struct alignas(16) DPrimWorld {
 // lies on plane l_axis = D + side * L.  The quads keep their own records (uv,
 // normals, material) for the hit record.
 constexpr uint32_t BOX_ENTRIES = 7;
-// f32 kernels test a sphere in f32 when |center| + |speed| + |r| stays within this (kernel.hpp
-// sphere_t_world), else in f64
+// f32 kernels test a sphere in f32 when its anchor P (the point nearest the world origin) plus
+// |speed| stays within this (kernel.hpp sphere_t_world_f32: any radius), else in f64
 constexpr double SPHERE_F32_EXTENT = 100.0;
 // PRIM_BOXY (world-list run kind only; header meta kind stays PRIM_BOX): a box turned
 // about the world y axis only.  Local axes (A, y, B): (N[0], N[2], D) = x, z entries

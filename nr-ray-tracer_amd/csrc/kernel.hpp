@@ -582,12 +582,12 @@ __device__ __forceinline__ float sphere_t_world_f32(const Q& q, const Ray<float>
     const float t = tn > 0.001f ? tn : tf;
     return ((disc >= 0.0f) & (t > 0.001f) & (t < INFINITY)) ? t : -1.0f;
 }
-// The world modes' sphere tests: f32 (above) for the world list's PRIM_SPHERE32 runs, spheres
-// within the scene's scale (AB[6] = 0: |center| + |speed| + |r| <= SPHERE_F32_EXTENT, flatten.cpp),
-// whose hit points the record then puts back on the surface (make_record_world); the quadratic in
-// f64 (below) for the large ones (the r = 1e5 and r = 1e3 ground spheres: their f32 hit points would
-// sit up to ~1e-5 off a surface of that size, and the next ray's t_min = 0.001 would not hide the
-// self-intersection), and for every sphere of a world-BVH leaf (world_prim_t).
+// The world modes' sphere tests: f32 (above) for the world list's PRIM_SPHERE32 runs, spheres whose
+// anchor lies within the scene's scale (AB[6] = 0: |P| + |speed| <= SPHERE_F32_EXTENT, flatten.cpp;
+// the r = 1e3 / 1e5 ground spheres included), whose hit points the record then puts back on the
+// surface with an anchored Newton step (make_record_world); the quadratic in f64 (below) for spheres
+// anchored far outside the scene (their e = o - P would not stay small), and for every sphere of a
+// world-BVH leaf (world_prim_t).
 template <class Q>
 __device__ __forceinline__ float sphere_t_world_f64(const Q& q, const Ray<float>& r) {
     DPrim<float> sp;
@@ -966,13 +966,22 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
 // lane's stack (LDS, entry k at stack[k * BLOCK]), so t_best shrinks early and
 // culls the far side.  The lanes of a wave descend until each holds a leaf (or
 // is done) before leaves are tested together ("while-while").
+#ifndef NRT_WBVH_SPHERE32
+// world-BVH leaf spheres: 2 = the anchored f32 quadratic only (the host keeps scenes with spheres
+// anchored outside the scene scale off the world BVH: flatten.cpp build_wbvh), 1 = f32 or f64 per
+// record (both compiled in: 131 VGPRs, 3 waves), 0 = f64 only (118 VGPRs)
+#define NRT_WBVH_SPHERE32 2
+#endif
 template <bool FLAT = false, bool TIE = false, int PRIMS = 0>  // PRIMS: WPRIMS_* of the scene's leaves
 __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const Ray<float>& ray, float t_best) {
     const uint32_t kind = q.meta & WKIND_MASK;  // BVH leaves hold spheres, quads and triangles only
     if (!FLAT && kind == PRIM_SPHERE) {  // FLAT: the scene has no spheres
-        // in f64: the f32 test of small spheres beside it took the generic world-BVH kernel to
-        // 129 VGPRs, 3 waves per SIMD (spheres.toml 1080p 34.9 -> 39.9 ms)
-        const float t = sphere_t_world_f64(q, ray);
+        // one sphere test compiled in (both took the generic world-BVH kernel to 129 VGPRs, 3 waves
+        // per SIMD: spheres.toml 1080p 34.9 -> 39.9 ms, round 3)
+        float t;
+        if constexpr (NRT_WBVH_SPHERE32 == 2) t = sphere_t_world_f32(q, ray);
+        else if constexpr (NRT_WBVH_SPHERE32 == 1) t = q.AB[6] == 0.0f ? sphere_t_world_f32(q, ray) : sphere_t_world_f64(q, ray);
+        else t = sphere_t_world_f64(q, ray);
         return (t >= 0.0f && t <= t_best) ? t : -1.0f;
     }
     const V<float> nrm = ld3(q.N);
@@ -1965,11 +1974,25 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
     h.p = pw;
     V<R> geo, shade;
     if (!FLAT && kind == PRIM_SPHERE) {
-        const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
-        geo = normalize(h.p - center);
-        // f32-tested spheres: the hit point back on the surface (its f32 t carries a few ulp, which
-        // would leave the next ray's origin off the surface by more than the t_min of 0.001 hides)
-        if (NRT_SPHERE_REPROJ && sizeof(R) == 4 && q.AB[6] == R(0)) h.p = center + fabs(q.D) * geo;
+        if (NRT_SPHERE_REPROJ && sizeof(R) == 4 && q.AB[6] == R(0)) {
+            // f32-tested spheres: the hit point back on the surface (its f32 t carries a few ulp,
+            // which would leave the next ray's origin off the surface by more than the t_min of
+            // 0.001 hides), as one Newton step on F(p) = |p - center|^2 - r^2 evaluated relative
+            // to the anchor P (F = |e|^2 + 2 e.V, e = p - P, V = P - center: small terms only, so
+            // the step is accurate for a ground sphere of r = 1e3 or 1e5 too, where center + r * n
+            // would round to the ulp of r)
+            const V<R> P = mk(q.AB[3], q.AB[4], q.AB[5]) + wray.time * ld3(q.AB);
+            const V<R> Vv = mk(q.S[0], q.S[1], q.S[2]);
+            const V<R> e = h.p - P;
+            const V<R> g = e + Vv;  // p - center
+            const R gg = dot(g, g);
+            const R F = dot(e, e) + R(2) * dot(e, Vv);
+            h.p = h.p - (F * fast_rcp(R(2) * gg)) * g;
+            geo = normalize(g);
+        } else {
+            const V<R> center = ld3(q.N) + wray.time * ld3(q.AB);
+            geo = normalize(h.p - center);
+        }
         shade = geo;
         // uv (acos / atan2) only where a texture reads it: sphere_uv, from the record's normal
         // (the ground sphere of the earth scene is solid: 18 % of its shading was this record)
