@@ -2358,7 +2358,10 @@ constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WBVH_WAVES
 #define NRT_WBVH_WAVES 1
 #endif
-    if (sizeof(R) == 4 && MAXD < 0 && !G::uses_lds) return NRT_WBVH_WAVES;
+#ifndef NRT_WBVH_SPHERE_WAVES
+#define NRT_WBVH_SPHERE_WAVES 5  // world BVH with spheres / textures (not KF_FLAT): 96 VGPRs, 5 spilled (spheres 1080p 32.5 -> 31.3 ms)
+#endif
+    if (sizeof(R) == 4 && MAXD < 0 && !G::uses_lds) return (kflags & KF_FLAT) ? NRT_WBVH_WAVES : NRT_WBVH_SPHERE_WAVES;
     if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT)) return NRT_FLAT_WAVES;
     return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
 }
