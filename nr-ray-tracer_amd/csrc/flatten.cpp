@@ -906,6 +906,11 @@ struct Flattener {
             const float v = std::strtof(e, nullptr);
             if (v > 0.0f && v < 100.0f) prim_cost = v;
         }
+        float sphere_cost = NRT_SPHERE_COST;  // knob NRT_SPHERE_COST (A/B runs)
+        if (const char* e = std::getenv("NRT_SPHERE_COST")) {
+            const float v = std::strtof(e, nullptr);
+            if (v > 0.0f && v < 100.0f) sphere_cost = v;
+        }
         std::vector<float> cost(out.wprims.size(), prim_cost);
         for (size_t i = 0; i < out.wprims.size(); ++i) {
             const DPrimWorld<double>& w = out.wprims[i];
@@ -922,7 +927,7 @@ struct Flattener {
                     out.wbvh_ok = false;
                     return;
                 }
-                cost[i] = NRT_SPHERE_COST * prim_cost;
+                cost[i] = sphere_cost * prim_cost;
                 for (int end = 0; end < 2; ++end)
                     for (int sg = -1; sg <= 1; sg += 2) {
                         double p[3];
