@@ -99,7 +99,7 @@ def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace, rng
     the unrolled code fuses a few operations differently, so a path can part at the ulp level:
     on the full C5 frame 3 of 1,048,576 pixels differ (scripts/jit_compare.py; with
     -ffp-contract=on the frames are identical and the kernel 3 % slower), and the spheres
-    scene (dielectrics, f64 sphere tests) parts on 0.2 % of its values at this size.  Bar:
+    scene (dielectrics) parts on 0.2 % of its values at this size.  Bar:
     >= 99 % of the values identical, channel means within 1 %."""
     s = load(scene, 40, 30, 64)
     if s.stats()["world_prims"] == 0 or (trace == "world-list" and not s.stats()["world_list_ok"]):
