@@ -2362,7 +2362,7 @@ constexpr int min_waves_per_simd(int kflags = 0) {
     if (sizeof(R) == 8 && SIG::lstack) return NRT_F64_LSTACK_WAVES;
     if (sizeof(R) == 8) return (kflags & KF_PLANES) ? NRT_F64_WAVES : NRT_F64_SPHERE_WAVES;
 #ifndef NRT_WBVH_WAVES
-#define NRT_WBVH_WAVES 1
+#define NRT_WBVH_WAVES 6  // KF_FLAT world BVH (teapot): 80 VGPRs, no spill (5 at the compiler's 81: C4 33.84 -> 33.60 ms)
 #endif
 #ifndef NRT_WBVH_SPHERE_WAVES
 #define NRT_WBVH_SPHERE_WAVES 5  // world BVH with spheres / textures (not KF_FLAT): 96 VGPRs, 5 spilled (spheres 1080p 32.5 -> 31.3 ms)
