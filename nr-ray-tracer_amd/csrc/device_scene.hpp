@@ -290,7 +290,10 @@ struct alignas(16) DMatFast {
 // of ceil(W / 8): rays that hit nearby points of a sphere read nearby texels in both directions,
 // so a line fetched for one serves its neighbours above and below as well (earth.toml: 4.96 GB
 // of HBM/MALL fetches per C3 launch with f32 row-major texels).
-enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1 };
+// RGB8T (default; NRT_TEX_RGB8=0 keeps RGBA8): the same bytes packed three per texel, tiles of 8 x 5 texels (120
+// bytes + 8 of padding, one 128-byte line): a line covers 40 texels instead of 32, at the cost of two
+// word loads and a byte align per lookup (tex_rgb8_byte; heights below 65536).
+enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1, TEXFMT_RGB8T = 2 };
 #if defined(__HIPCC_RTC__)
 #define NRT_HD __device__
 #elif defined(__HIPCC__)
@@ -300,6 +303,11 @@ enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1 };
 #endif
 NRT_HD inline uint64_t tex_tiled_index(uint32_t x, uint32_t y, uint32_t tiles_per_row) {
     return ((uint64_t)(y >> 2) * tiles_per_row + (x >> 3)) * 32u + (y & 3u) * 8u + (x & 7u);
+}
+// RGB8T: byte offset of texel (x, y) (y < 65536: y / 5 as (y * 52429) >> 18, exact there)
+NRT_HD inline uint64_t tex_rgb8_byte(uint32_t x, uint32_t y, uint32_t tiles_per_row) {
+    const uint32_t ty = (y * 52429u) >> 18, ly = y - 5u * ty;
+    return ((uint64_t)ty * tiles_per_row + (x >> 3)) * 128u + (ly * 8u + (x & 7u)) * 3u;
 }
 struct alignas(16) DTexture {
     uint32_t kind;

@@ -43,8 +43,13 @@ constexpr int BLOCK = 256;
 #ifndef NRT_WBVH_IFIF
 // world BVH: one node visit or one primitive per lane and trip (wbvh_trip) in the KF_FLAT
 // variant (triangles / quads only: a primitive costs a fifth of a visit; C4 6 307 -> 6 400
-// Msamples/s); scenes with f64 sphere tests keep the speculative rounds (C1 -27 % if-if)
+// Msamples/s); scenes with f64 sphere tests kept the speculative rounds (C1 -27 % if-if, round 2);
+// with the f32 sphere test the sphere / texture variant takes the trips too (NRT_WBVH_IFIF_SPHERES:
+// spheres 1080p 31.1 -> 30.7 ms, round 3)
 #define NRT_WBVH_IFIF 1
+#endif
+#ifndef NRT_WBVH_IFIF_SPHERES
+#define NRT_WBVH_IFIF_SPHERES 1
 #endif
 #ifndef NRT_SPHERE_REPROJ
 #define NRT_SPHERE_REPROJ 1  // f32-tested spheres: hit points put back on the surface (make_record_world)
@@ -1398,12 +1403,12 @@ template <typename R, bool FLAT = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ void wbvh_step(WbvhTrav& ts, const DSceneView<R>& sc, const Ray<float>& ray, STKP stack,
                                           unsigned long long* pc = nullptr) {
     if constexpr (SIG::bvh != 0) {  // a scene-specialised kernel (jit.hip)
-        if constexpr (FLAT && NRT_WBVH_IFIF)
+        if constexpr ((FLAT || NRT_WBVH_IFIF_SPHERES) && NRT_WBVH_IFIF)
             wbvh_trip_impl<R, SIG::bvh, FLAT, SIG::tie, SIG::prims>(ts, sc, ray, stack, pc);
         else wbvh_round_impl<R, SIG::bvh, FLAT>(ts, sc, ray, stack, pc);
         return;
     }
-    if constexpr (FLAT && NRT_WBVH_IFIF) {
+    if constexpr ((FLAT || NRT_WBVH_IFIF_SPHERES) && NRT_WBVH_IFIF) {
         if (sc.wbvh4) wbvh_trip<R, 4, FLAT>(ts, sc, ray, stack, pc);
         else wbvh_trip<R, 2, FLAT>(ts, sc, ray, stack, pc);
     } else {
@@ -2170,7 +2175,7 @@ __device__ __forceinline__ double perlin_texture(const uint32_t* texels, const D
 // product alone is 1 ulp off for 158 of them); explicit FMAs, so the exact kernel's
 // -ffp-contract=off build computes the same
 #ifndef NRT_TEX_FORMATS
-#define NRT_TEX_FORMATS 3  // image texel formats compiled in: 1 RGB32F, 2 RGBA8 (A/B via NRT_JIT_DEFS)
+#define NRT_TEX_FORMATS 7  // image texel formats compiled in: 1 RGB32F, 2 RGBA8, 4 RGB8T (A/B via NRT_JIT_DEFS)
 #endif
 __device__ __forceinline__ float unorm8(uint32_t k) {
     constexpr float r = 1.0f / 255.0f;
@@ -2204,6 +2209,13 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
             // reference (Q12): clamped to the last texel here.
             uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
             uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)t.b ? t.b - 1 : (uint32_t)fy);
+            if ((NRT_TEX_FORMATS & 4) && t.format == TEXFMT_RGB8T) {
+                // three bytes at a byte offset: the two words that hold them, aligned (v_alignbyte)
+                const uint64_t o = tex_rgb8_byte(x, y, (t.a + 7u) >> 3);
+                const uint32_t* pw = sc.texels + t.offset + (o >> 2);
+                const uint32_t w = __builtin_amdgcn_alignbyte(pw[1], pw[0], (uint32_t)o & 3u);
+                return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
+            }
             if ((NRT_TEX_FORMATS & 2) && (!(NRT_TEX_FORMATS & 1) || t.format == TEXFMT_RGBA8)) {
                 // one word (8 x 4 tiles): the three bytes, k / 255.0f exactly
 #ifdef NRT_TEX_ROWMAJOR

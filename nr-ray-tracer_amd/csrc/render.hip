@@ -249,7 +249,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     hipStream_t stream = (hipStream_t)stream_ptr;
     RenderParams q = p;
     if (q.wave_wait == 0)  // if-if trips (KF_FLAT world BVH) shade at 24 finished lanes (C4 34.6 -> 34.3 ms),
-        q.wave_wait = ds->flat ? 24u : 32u;  // the speculative rounds at 32 (spheres.toml 1080p 34.6 -> 33.9 ms)
+        q.wave_wait = ds->flat ? 24u : 32u;  // the sphere / texture variant at 32 (spheres.toml 1080p: 31.06 ms at 24, 30.71 at 32)
     {  // Philox: group queue heads; ChaCha8: the pixel counter of the persistent lanes (head 0)
         const size_t qwords = (size_t)QUEUE_HEADS * QUEUE_STRIDE;
         q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;

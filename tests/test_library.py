@@ -183,10 +183,12 @@ def test_library_built_from_these_sources():
     # the same two with the reference's ChaCha8 stream (one lane per pixel)
     "float, nrt::dev::ChaCha8, 0, false, true, 4, nrt::dev::WorldSig<23u, 21u, 40u>",
     "float, nrt::dev::ChaCha8, -1, false, false, 4, nrt::dev::BvhSig<4, false>",
-    # the teapot's compact tree (16-bit refs, triangles only: LDS node cache) and the earth's
-    # world list (one f64 sphere run, one f32 sphere run; not KF_FLAT)
+    # the teapot's compact tree (16-bit refs, triangles only: LDS node cache), a world list with
+    # an f64 and an f32 sphere run (a sphere anchored outside the scene scale beside one inside),
+    # and the earth's world list (one f32 sphere run; not KF_FLAT)
     "float, nrt::dev::Philox, -1, false, false, 4, nrt::dev::BvhSig<5, false, 2>",
     "float, nrt::dev::Philox, 0, false, true, 0, nrt::dev::WorldSig<16u, 41u>",
+    "float, nrt::dev::Philox, 0, false, true, 0, nrt::dev::WorldSig<57u>",
 ])
 def test_scene_specialised_kernel_compiles(targs):
     """The device headers embedded in libnrt.so still compile under hiprtc (jit.hip), so a GPU

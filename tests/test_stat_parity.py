@@ -134,7 +134,7 @@ VARIANTS = [
     ("teapot_32", "f32", "philox", "auto", 65536),         # world BVH (C4's kernel)
     ("teapot_32", "f32", "philox", "bvh", 16384),
     ("teapot_32", "f64", "philox", "auto", 16384),
-    ("earth_48", "f32", "philox", "auto", 65536),         # image textures, f64 spheres
+    ("earth_48", "f32", "philox", "auto", 65536),         # image textures, f32 spheres (r = 1000 ground)
     ("earth_48", "f32", "chacha8", "auto", 4096),
 ]
 
