@@ -1677,6 +1677,9 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
 // at the bound raised by 2^-20 as there.  A lane with more than XCAND live candidates at once
 // (never seen on the reference scenes) falls back to trace_exact_wbvh.
 constexpr int XCAND = 4;
+#ifndef NRT_PF_RCP
+#define NRT_PF_RCP 1
+#endif
 #ifndef NRT_EXACT_IFIF
 #define NRT_EXACT_IFIF 0  // the prefiltered compact walk as if-if trips (A/B build)
 #endif
@@ -1695,9 +1698,19 @@ __device__ __forceinline__ bool exact_prefilter(const DPrimWorld<float>& q, cons
     thi = INFINITY;
     if (aden + eden < 1e-8f) return false;           // |n.d| < 1e-8: the reference rejects it
     if (!(aden - 2.0f * eden > 1e-8f)) return true;  // near-parallel (or NaN): a candidate
+#if NRT_PF_RCP
+    // hardware reciprocals (1 ulp) instead of IEEE divisions (the exact kernel's build has no fast
+    // division): t carries ~2 ulp more, far inside E * |t|; the quotient of the bound is raised
+    // by 2^-20 to stay an upper bound
+    const float t = (q.D - dot(N, r.o)) * __builtin_amdgcn_rcpf(den);
+    const float at = fabsf(t);
+    const float et = (E * (fabsf(q.D) + absdot(N, r.o)) + at * eden) * __builtin_amdgcn_rcpf(aden - eden) *
+                         (1.0f + 0x1p-20f) + E * at;
+#else
     const float t = (q.D - dot(N, r.o)) / den;
     const float at = fabsf(t);
     const float et = (E * (fabsf(q.D) + absdot(N, r.o)) + at * eden) / (aden - eden) + E * at;
+#endif
     if (t + et < 0.001f) return false;  // t < 0.001
     const V<float> P = mk(fabsf(r.o.x) + at * fabsf(r.d.x), fabsf(r.o.y) + at * fabsf(r.d.y),
                           fabsf(r.o.z) + at * fabsf(r.d.z));  // bounds |o + t d| per axis
