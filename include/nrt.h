@@ -131,7 +131,7 @@ typedef struct {
     uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
                                 (else AUTO takes the world BVH, which compares tie keys) */
     uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
-    uint32_t texel_bytes;    /* HBM bytes of the texel array (RGBA8 images: 4 B per texel) */
+    uint32_t texel_bytes;    /* HBM bytes of the texel array (file images: 3 B per texel in 128-B tiles of 8 x 5) */
 } nrt_scene_stats;
 /* Exact-kernel traversal (same closest hit and tie-break as BVH::hit, object.rs:89-121):
  *   BVH      the reference tree, box by box

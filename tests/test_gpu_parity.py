@@ -361,6 +361,18 @@ def test_jit_require_refuses_the_generic_fallback(monkeypatch):
     assert nrt.jit_stats()["launches"] == before["launches"]  # the generic kernel rendered
 
 
+@pytest.mark.parametrize("defs", ["-DNRT_SLOTS_LIST=4", "-DNRT_SLOTS_BVH=8"])
+def test_jit_defs_refuse_layout_macros(monkeypatch, defs):
+    """NRT_JIT_DEFS (an A/B tuning knob) may not change the Philox pool's LDS layout: the host sizes
+    the allocation from the library's own build (philox_pool_bytes), so a specialised kernel with
+    more slots would write past it (jit.hip refuses the render call instead)."""
+    s = load("scenes/cornell-box-scene.json", 32, 24, 2)
+    monkeypatch.setenv("NRT_JIT_DEFS", defs)
+    monkeypatch.setenv("NRT_JIT", "1")
+    with pytest.raises(nrt.NrtError, match="LDS layout"):
+        s.render(precision="f32", rng="philox", trace="world-list" if "LIST" in defs else "auto")
+
+
 def test_exact_world_mode_far_camera(monkeypatch):
     """The exact world mode culls with f32 boxes padded by 1e-6 of the scene's extent, enough for
     ray origins within ~7x that extent; a camera farther out makes make_params (api.cpp) take the
