@@ -591,8 +591,8 @@ __device__ __forceinline__ float sphere_t_world_f32(const Q& q, const Ray<float>
 // anchor lies within the scene's scale (AB[6] = 0: |P| + |speed| <= SPHERE_F32_EXTENT, flatten.cpp;
 // the r = 1e3 / 1e5 ground spheres included), whose hit points the record then puts back on the
 // surface with an anchored Newton step (make_record_world); the quadratic in f64 (below) for spheres
-// anchored far outside the scene (their e = o - P would not stay small), and for every sphere of a
-// world-BVH leaf (world_prim_t).
+// anchored far outside the scene (their e = o - P would not stay small; such a scene stays off the
+// world BVH, whose leaves compile the f32 test only: world_prim_t).
 template <class Q>
 __device__ __forceinline__ float sphere_t_world_f64(const Q& q, const Ray<float>& r) {
     DPrim<float> sp;
