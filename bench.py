@@ -164,16 +164,34 @@ def load_pmc(key):
 
 def load_work(scene, w, h, spp=None):
     """Per-sample algorithmic work of this config (tests/golden/work_counts.json), or None.
-    Per-sample counts do not depend on spp (samples of a pixel are independent)."""
+    Per-sample counts do not depend on spp (samples of a pixel are independent).  Another image size of
+    a counted scene (same camera, the view sampled more or less densely) takes that scene's counts and
+    says so in `counted_at`."""
     path = os.path.join(ROOT, "tests", "golden", "work_counts.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
         wc = json.load(fh)
+    same_scene = None
     for name, c in wc["configs"].items():
         if c["scene"] == scene and c["width"] == w and c["height"] == h:
             return dict(c, name=name)
-    return None
+        if c["scene"] == scene and same_scene is None:
+            same_scene = dict(c, name=name, counted_at=f"{c['width']}x{c['height']}")
+    return same_scene
+
+
+# texel payload per format (device_scene.hpp TEXFMT_*): file images are 3 bytes per texel in 128-B
+# lines of 8 x 5 (3.2 B stored per texel with the line padding), RGBA8 words, or f32 RGB
+TEXEL_PAYLOAD = ((3.2, 3), (4.0, 4), (12.0, 12))
+
+
+def texel_payload_bytes(stats):
+    """Bytes per texel as stored (3 / 4 / 12), from the texel array's bytes per texel."""
+    if not stats.get("texels"):
+        return 0
+    per = stats["texel_bytes"] / stats["texels"]
+    return min(TEXEL_PAYLOAD, key=lambda fp: abs(fp[0] - per))[1]
 
 
 def work_block(wc, msamples_per_s, precision):
@@ -186,7 +204,8 @@ def work_block(wc, msamples_per_s, precision):
             "rays_per_sample": wc["rays_per_sample"], "flops_per_sample": wc["flops_per_sample"],
             "algorithmic_tflops": round(tflops, 3), "valu_peak_tflops": VALU_PEAK_TFLOPS[precision],
             "valu_flop_frac": round(tflops / VALU_PEAK_TFLOPS[precision], 4),
-            "source": f"tests/golden/work_counts.json[{wc['name']}] (oracle event counts, ChaCha8 stream)"}
+            "source": f"tests/golden/work_counts.json[{wc['name']}] (oracle event counts, ChaCha8 stream"
+                      + (f"; counted at {wc['counted_at']}, the same view)" if wc.get("counted_at") else ")")}
 
 
 # ------------------------------------------------------------------ main
@@ -234,10 +253,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # every rank runs the scene-specialised kernel or none renders: a rank on the generic kernel
-        # (FMA contraction can part at the ulp level) would make the frame differ from N = 1's
-        os.environ.setdefault("NRT_JIT", "require")
     if world != args.gpus and world == 1:
         raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
     ndev = torch.cuda.device_count()
@@ -335,8 +350,7 @@ def main():
     mixed = False
     if world > 1:
         # max over ranks of the times; min and max over ranks of "timed on the scene-specialised kernel"
-        # (its f32 frames may differ in the last bits from the generic kernel's: a mix would make the
-        # assembled frame depend on which rank's hiprtc build failed)
+        # (the generic kernel renders the same bits, kernel.hpp fmad, but slower: a mix is reported)
         t = torch.tensor([elapsed, kern_ms, float(specialised), -float(specialised)], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -357,13 +371,22 @@ def main():
         samples = float(W) * H * spp
         value = samples * args.steps / elapsed / 1e6
         st = scene.stats()
-        alg_bytes = rows * W * 12 + scene_bytes(st, args.precision)
-        hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         key = {"scene": args.scene, "width": W, "height": H, "spp": spp, "precision": args.precision,
                "rng": args.rng, "trace": args.trace, "n_gpus": world}
         pmc = load_pmc(key)
         traffic = pmc.get("hbm_bytes_per_launch")
         wc = load_work(args.scene, W, H, spp)
+        # SURVEY §8(d) bytes per sample: 12/spp of framebuffer + texel_fetches/sample x the texel's bytes,
+        # priced at the bytes per texel actually stored (3 for file images); the scene's records are a
+        # cache-resident working set, listed beside it (scene_bytes)
+        fb_bytes = rows * W * 12
+        texel_b = texel_payload_bytes(st)
+        fetches = 0.0 if wc is None else wc["per_sample"].get("texel_fetches", 0.0)
+        tex_bytes = fetches * texel_b * rows * W * spp
+        alg_bytes = fb_bytes + tex_bytes
+        hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        prof_s = pmc.get("avg_ns", 0) / 1e9 if pmc else 0
+        counter_gbs = traffic / prof_s / 1e9 if traffic and prof_s else None
         peak = VALU_PEAK_TFLOPS[args.precision]
         if wc is not None:
             flops_launch = wc["flops_per_sample"] * rows * W * spp  # this rank's launch
@@ -393,13 +416,24 @@ def main():
                 f"tests/golden/work_counts.json[{wc['name']}]: {wc['flops_per_sample']} algorithmic FLOPs/sample "
                 f"(oracle event counts x SURVEY §8(d) per-event costs) x {rows * W * spp} samples per launch",
                 "hbm": {"achieved": round(hbm_achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": alg_bytes,
-                        "traffic": traffic},
+                        "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": round(alg_bytes),
+                        "algorithmic_bytes": {"framebuffer": fb_bytes, "texels": round(tex_bytes),
+                                              "texel_fetches_per_sample": fetches, "bytes_per_texel": texel_b,
+                                              "source": "SURVEY §8(d): 12/spp + texel_fetches x bytes per "
+                                                        "texel as stored, per sample"},
+                        "scene_bytes": scene_bytes(st, args.precision),
+                        "traffic": traffic,
+                        # rocprofv3 FETCH_SIZE + WRITE_SIZE per launch over the profiled kernel time
+                        # (profiles/pmc_summary.json, the committed profile of this variant and config)
+                        "counter_gbs": None if counter_gbs is None else round(counter_gbs, 3),
+                        "counter_frac": None if counter_gbs is None else counter_gbs / HBM_PEAK_GBS,
+                        "traffic_over_algorithmic": None if not traffic else round(traffic / alg_bytes, 3)},
                 "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
                                                 "valu_busy_est", "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
                                                 "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
                 "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
-                        "divergence; its HBM traffic is the framebuffer plus a few KB of scene"},
+                        "divergence; its compulsory HBM traffic is the framebuffer (plus texel fetches in textured "
+                        "scenes)"},
             "work": work_block(wc, value, args.precision),
             "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
                            "frame_wall": round(elapsed / args.steps * 1e3, 3)},

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 4
+#define NRT_ABI_VERSION 5
 
 enum {
     NRT_OK = 0,
@@ -131,7 +131,8 @@ typedef struct {
     uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
                                 (else AUTO takes the world BVH, which compares tie keys) */
     uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
-    uint32_t texel_bytes;    /* HBM bytes of the texel array (file images: 3 B per texel in 128-B tiles of 8 x 5) */
+    uint32_t reserved;
+    uint64_t texel_bytes;    /* HBM bytes of the texel array (file images: 3 B per texel in 128-B tiles of 8 x 5) */
 } nrt_scene_stats;
 /* Exact-kernel traversal (same closest hit and tie-break as BVH::hit, object.rs:89-121):
  *   BVH      the reference tree, box by box
@@ -188,6 +189,22 @@ int32_t nrt_texture_solid(nrt_builder* b, const double color[3]);               
 int32_t nrt_texture_image(nrt_builder* b, uint32_t w, uint32_t h, const float* rgb);   /* Image (Rgb32F texels) */
 int32_t nrt_texture_image_file(nrt_builder* b, const char* path);                      /* Image::try_from_path */
 int32_t nrt_texture_checker(nrt_builder* b, int32_t even, int32_t odd, double scale);  /* CheckerBuilder */
+/* PerlinRidgedNoiseBuilder (lib/textures/noise.rs:30-101) and MarbleBuilder (lib/textures/marble.rs:24-60):
+ * each builder field is an Option, present when its NRT_NOISE_* bit is set in `set`; absent fields take the
+ * builder's defaults (seed 0; octaves 1, clamped to [1, 32] by Fbm::set_octaves; frequency 1; lacunarity
+ * 2*pi/3; persistence 0.5; Marble: 7 octaves and the default lacunarity / persistence, only seed and
+ * frequency read).  get_color: |Fbm<Perlin>|(p) (Noise), (1 + sin(frequency * p.z + 10 |Fbm|(p))) / 2
+ * (Marble), grey, at the world-space hit point. */
+enum {
+    NRT_NOISE_SEED = 1u << 0,
+    NRT_NOISE_OCTAVES = 1u << 1,
+    NRT_NOISE_FREQUENCY = 1u << 2,
+    NRT_NOISE_LACUNARITY = 1u << 3,
+    NRT_NOISE_PERSISTENCE = 1u << 4
+};
+int32_t nrt_texture_noise(nrt_builder* b, uint32_t set, uint32_t seed, uint64_t octaves, double frequency,
+                          double lacunarity, double persistence);
+int32_t nrt_texture_marble(nrt_builder* b, uint32_t set, uint32_t seed, double frequency);
 int32_t nrt_material_lambertian(nrt_builder* b, int32_t texture);                       /* Lambertian::with_texture */
 int32_t nrt_material_metal(nrt_builder* b, double fuzz, int32_t texture);               /* MetalBuilder */
 int32_t nrt_material_dielectric(nrt_builder* b, double refraction_index);               /* Dielectric::new */

@@ -462,6 +462,24 @@ int32_t nrt_texture_checker(nrt_builder* b, int32_t even, int32_t odd, double sc
     NRT_BUILD(auto t = std::make_shared<Texture>(); t->kind = Texture::Checker; t->even = tex_at(b, even);
               t->odd = tex_at(b, odd); t->scale = scale; return add_tex(b, t);)
 }
+int32_t nrt_texture_noise(nrt_builder* b, uint32_t set, uint32_t seed, uint64_t octaves, double frequency,
+                          double lacunarity, double persistence) {
+    // PerlinRidgedNoiseBuilder::build (noise.rs:79-101), as the loader's Noise texture (scene_config.cpp)
+    NRT_BUILD(if (set & ~0x1Fu) throw std::invalid_argument("unknown NRT_NOISE_* bits"); FbmParams f;
+              if (set & NRT_NOISE_SEED) f.seed = seed; if (set & NRT_NOISE_FREQUENCY) f.frequency = frequency;
+              if (set & NRT_NOISE_LACUNARITY) f.lacunarity = lacunarity;
+              if (set & NRT_NOISE_PERSISTENCE) f.persistence = persistence;
+              const uint64_t oct = (set & NRT_NOISE_OCTAVES) ? octaves : 1u; f.octaves = fbm_octaves(oct);
+              auto t = std::make_shared<Texture>(); t->kind = Texture::Noise; t->fbm = f; return add_tex(b, t);)
+}
+int32_t nrt_texture_marble(nrt_builder* b, uint32_t set, uint32_t seed, double frequency) {
+    // MarbleBuilder::build (marble.rs:46-60): only seed and frequency; 7 octaves
+    NRT_BUILD(if (set & ~(uint32_t)(NRT_NOISE_SEED | NRT_NOISE_FREQUENCY))
+                  throw std::invalid_argument("Marble takes only NRT_NOISE_SEED and NRT_NOISE_FREQUENCY");
+              FbmParams f; if (set & NRT_NOISE_SEED) f.seed = seed; if (set & NRT_NOISE_FREQUENCY) f.frequency = frequency;
+              f.octaves = MARBLE_OCTAVES; auto t = std::make_shared<Texture>(); t->kind = Texture::Marble; t->fbm = f;
+              return add_tex(b, t);)
+}
 int32_t nrt_material_lambertian(nrt_builder* b, int32_t texture) {
     NRT_BUILD(auto m = std::make_shared<Material>(); m->kind = Material::Lambertian; m->texture = tex_at(b, texture);
               return add_mat(b, m);)
@@ -614,7 +632,8 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
         out->coplanar_pairs = f.coplanar_pairs;
         out->world_list_ok = f.world_ok && f.list_ok ? 1u : 0u;
         out->exact_mode = exact_mode(f);
-        out->texel_bytes = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, f.texels.size() * sizeof(uint32_t));
+        out->reserved = 0;
+        out->texel_bytes = (uint64_t)f.texels.size() * sizeof(uint32_t);
         return NRT_OK;
     });
 }

@@ -270,6 +270,7 @@ int main(int argc, char** argv) {
             opts.rng = r == "philox" ? NRT_RNG_PHILOX : r == "chacha8" ? NRT_RNG_CHACHA8 : 99;
             if (opts.rng == 99) die("--rng must be chacha8 or philox");
         } else if (a == "--gpus") gpus = atoi(val().c_str());
+        else if (a == "--legacy-schema") load_flags |= NRT_LOAD_LEGACY_SCHEMA;  // a switch: takes no value
         else if (a.rfind("--", 0) == 0) kv.emplace_back(a, val());
         else if (scene.empty()) scene = a;
         else usage();

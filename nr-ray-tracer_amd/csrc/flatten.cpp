@@ -931,6 +931,7 @@ struct Flattener {
             if (v > 0.0f && v < 100.0f) sphere_cost = v;
         }
         std::vector<float> cost(out.wprims.size(), prim_cost);
+        bool far_sphere = false;
         for (size_t i = 0; i < out.wprims.size(); ++i) {
             const DPrimWorld<double>& w = out.wprims[i];
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -941,11 +942,9 @@ struct Flattener {
             if (kind == PRIM_SPHERE) {  // center(t) = N + t * speed, t in [0, 1]
                 // the f32 kernels' world-BVH leaves test spheres in f32 only (kernel.hpp world_prim_t,
                 // the anchored quadratic): a sphere anchored outside the scene scale leaves the
-                // scene to the instance BVH
-                if (w.AB[6] != 0.0) {
-                    out.wbvh_ok = false;
-                    return;
-                }
+                // scene's f32 renders to the instance BVH (wbvh_f32_ok); the tree is still built, for
+                // the exact kernel's culling walk, which tests every primitive in f64
+                if (w.AB[6] != 0.0) far_sphere = true;
                 cost[i] = sphere_cost * prim_cost;
                 for (int end = 0; end < 2; ++end)
                     for (int sg = -1; sg <= 1; sg += 2) {
@@ -983,6 +982,7 @@ struct Flattener {
         out.wbvh_prims.reserve(out.wbvh.order.size());
         for (uint32_t idx : out.wbvh.order) out.wbvh_prims.push_back(out.wprims[idx]);
         out.wbvh_ok = true;
+        out.wbvh_f32_ok = !far_sphere;
     }
 
     // DXform of a transform node (every chain was emitted by instance()).

@@ -39,7 +39,8 @@ struct FlatScene {
     // World BVH over the (unfused) world primitives, for large flattenable scenes.
     WorldBvh wbvh;
     std::vector<DPrimWorld<double>> wbvh_prims;  // BVH leaf order
-    bool wbvh_ok = false;
+    bool wbvh_ok = false;      // the tree is built (the exact kernel's culling walk may use it)
+    bool wbvh_f32_ok = false;  // ... and the f32 world-BVH kernels may: every sphere anchored within the scene
     // Exact kernel's world-BVH mode: the tree it culls with and the exact reference of each of
     // its slots (device_scene.hpp DExactRef), when every world primitive maps onto the exact
     // tree's depth-first walk (instances not nested).  Scenes whose primitives sit under

@@ -87,6 +87,18 @@ template <typename R> __device__ __forceinline__ V<R> normalize(V<R> a) {
 template <> __device__ __forceinline__ V<float> normalize<float>(V<float> a) {
     return __builtin_amdgcn_rsqf(dot(a, a)) * a;
 }
+// a * b + c, fused (one rounding) in f32.  The fast kernels are compiled with -ffp-contract=on
+// (Makefile FAST_CONTRACT, the same for kernels_fast.o and the hiprtc build, jit.hip): only
+// `a * b + c` written as one expression fuses, so the generic and the scene-specialised
+// kernels round alike whatever the inliner and unroller make of the code around it (with
+// -ffp-contract=fast the backend fuses across statements depending on code shape, and the two
+// kernels parted on 3 of 1 048 576 C5 pixels).  The products the vector helpers below hand to
+// a sum are fused here explicitly.  f64: unfused in the exact TU (-ffp-contract=off).
+template <typename R> __device__ __forceinline__ R fmad(R a, R b, R c) { return a * b + c; }
+template <> __device__ __forceinline__ float fmad<float>(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+template <typename R> __device__ __forceinline__ V<R> vfma(R s, V<R> a, V<R> b) {  // s * a + b
+    return {fmad(s, a.x, b.x), fmad(s, a.y, b.y), fmad(s, a.z, b.z)};
+}
 template <typename R> __device__ __forceinline__ V<R> ld3(const R* p) { return {p[0], p[1], p[2]}; }
 template <typename R> __device__ __forceinline__ V<R> ld3d(const double* p) { return {(R)p[0], (R)p[1], (R)p[2]}; }
 
@@ -420,14 +432,15 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_di
 // p uniform in the unit ball, p/|p|^2 = u/r with u uniform on the sphere and
 // r = U^(1/3); p uniform in the unit disk, p/|p|^2 = (cos t, sin t)/sqrt(U).
 template <typename R> __device__ __forceinline__ V<R> unit_ball_inverse(uint32_t w0, uint32_t w1, uint32_t w2) {
-    const R z = R(2) * u01<R>(w0) - R(1);
+    const R z = fmad(R(2), u01<R>(w0), R(-1));
     const R turn = u01<R>(w1);
     const R w = R(1) - u01<R>(w2);  // (0, 1]
     const R s = fast_sqrt(fmax(R(0), R(1) - z * z));  // f32: v_sqrt_f32 (1 ulp)
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_exp2f(-0.333333343f * __builtin_amdgcn_logf(w));
         const float c = __builtin_amdgcn_cosf(turn), sn = __builtin_amdgcn_sinf(turn);  // argument in turns
-        return (inv_r * s) * mk(c, sn, R(0)) + mk(R(0), R(0), inv_r * z);
+        const float k = inv_r * s;
+        return mk(k * c, k * sn, inv_r * z);
     } else {
         double sn, c;
         sincospi(2.0 * turn, &sn, &c);
@@ -528,7 +541,7 @@ __device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alph
     if (fabs(denom) < R(1e-8)) return R(-1);
     const R t = fast_div(q.s - dot(nrm, r.o), denom);
     if (!(R(0.001) <= t && t <= R(INFINITY))) return R(-1);
-    point = r.o + t * r.d;
+    point = vfma(t, r.d, r.o);
     const V<R> ph = point - ld3(q.a);
     alpha = dot(ld3(q.w), cross(ph, ld3(q.c)));
     beta = dot(ld3(q.w), cross(ld3(q.b), ph));
@@ -554,7 +567,7 @@ __device__ __forceinline__ R fast_prim_t(const DPrimFast<R>& q, const Ray<R>& r,
     const V<R> n = ld3(q.n);
     const R denom = dot(n, r.d);
     const R t = (q.d - dot(n, r.o)) * fast_rcp(denom);
-    const V<R> p = r.o + t * r.d;
+    const V<R> p = vfma(t, r.d, r.o);
     const R alpha = dot(p, ld3(q.A)) - q.a0;
     const R beta = dot(p, ld3(q.B)) - q.b0;
     const bool quad_in = (alpha >= R(0) && alpha <= R(1)) && (beta >= R(0) && beta <= R(1));
@@ -779,7 +792,7 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
             const f32x2 lb = dox * q->AB[0] + doz * q->AB[2];
             const float ia = __builtin_amdgcn_rcpf(la.x), ib = __builtin_amdgcn_rcpf(lb.x);
             const float ax = (q->D - la.y) * ia, az = (q->AB[3] - lb.y) * ib;
-            const float bx = ax + ia, bz = az + ib;
+            const float bx = __builtin_fmaf(q->D - la.y, ia, ia), bz = __builtin_fmaf(q->AB[3] - lb.y, ib, ib);
             const float ay = __builtin_fmaf(q->AB[4], inv[1], -oinv[1]), by = __builtin_fmaf(q->AB[5], inv[1], -oinv[1]);
             const float nx = fminf(ax, bx), ny = fminf(ay, by), nz = fminf(az, bz);
             const float fx = fmaxf(ax, bx), fy = fmaxf(ay, by), fz = fmaxf(az, bz);
@@ -813,7 +826,9 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
                         iz = __builtin_amdgcn_rcpf(lz.x);
             const float ax = (q->D - lx.y) * ix, ay = (q->AB[3] - ly.y) * iy, az = (q->AB[7] - lz.y) * iz;
             // planes l = D and l = D + L per local axis (L_a in S[a]; flatten.cpp fuse_box)
-            const float bx = ax + ix, by = ay + iy, bz = az + iz;  // planes x' = 0 and x' = 1
+            // planes x' = 0 and x' = 1
+            const float bx = __builtin_fmaf(q->D - lx.y, ix, ix), by = __builtin_fmaf(q->AB[3] - ly.y, iy, iy),
+                        bz = __builtin_fmaf(q->AB[7] - lz.y, iz, iz);
             const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
             const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
             // entry face unless it lies before t_min (origin on or inside the box): then the exit face
@@ -992,7 +1007,7 @@ __device__ __forceinline__ float world_prim_t(const DPrimWorld<float>& q, const 
     const V<float> nrm = ld3(q.N);
     const float denom = dot(nrm, ray.d);
     const float t = (q.D - dot(nrm, ray.o)) * __builtin_amdgcn_rcpf(denom);
-    const V<float> pt = ray.o + t * ray.d;
+    const V<float> pt = vfma(t, ray.d, ray.o);
     const float alpha = dot(pt, mk(q.AB[0], q.AB[2], q.AB[4])) - q.AB[6];
     const float beta = dot(pt, mk(q.AB[1], q.AB[3], q.AB[5])) - q.AB[7];
     const float lo = fminf(alpha, beta);
@@ -1992,7 +2007,7 @@ __device__ __forceinline__ Rec<R> make_record_world(const DSceneView<R>& sc, con
         const uint32_t cls = q.meta >> WCLASS_SHIFT;
         t = cls == WCLASS_WIN ? t * R(1.0 / (1.0 - (double)WTIE_EPS)) : (cls == WCLASS_LOSE ? t * R(1.0 / (1.0 + (double)WTIE_EPS)) : t);
     }
-    const V<R> pw = wray.o + t * wray.d;
+    const V<R> pw = vfma(t, wray.d, wray.o);
     const uint32_t kind = q.meta & WKIND_MASK;
     Rec<R> h;
     h.p = pw;
@@ -2063,7 +2078,7 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     const R t = hm.t;
     if constexpr (!EXACT) {
         const DPrimFast<R>& q = sc.fprims[hm.prim];
-        h.p = ray.o + t * ray.d;
+        h.p = vfma(t, ray.d, ray.o);
         if (q.kind == PRIM_SPHERE) {
             const V<R> center = ld3(q.n) + ray.time * ld3(q.A);
             outward = normalize(h.p - center);
@@ -2083,14 +2098,14 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
     } else if (!PLANES && pr.kind == PRIM_SPHERE) {  // sphere.rs:148-161 (f64 acos / atan2: 50 VGPRs of
                                                     // spills in the plane-only variant, were it compiled in)
         const V<R> center = ld3(pr.a) + ray.time * ld3(pr.b);
-        h.p = ray.o + t * ray.d;
+        h.p = vfma(t, ray.d, ray.o);
         outward = normalize(h.p - center);
         const R theta = acos(-outward.y);
         const R phi = atan2(-outward.z, outward.x) + R(M_PI);
         h.u = phi / (R(2.0) * R(M_PI));
         h.v = theta / R(M_PI);
     } else {  // plane.rs:156-159
-        h.p = ray.o + t * ray.d;
+        h.p = vfma(t, ray.d, ray.o);
         const V<R> ph = h.p - ld3(pr.a);
         h.u = dot(ld3(pr.w), cross(ph, ld3(pr.c)));
         h.v = dot(ld3(pr.w), cross(ld3(pr.b), ph));
@@ -2251,12 +2266,12 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
 }
 
 template <typename R> __device__ __forceinline__ V<R> reflect(V<R> v, V<R> n) {
-    return v - ((R(2.0) * dot(v, n)) * n);
+    return vfma(-(R(2.0) * dot(v, n)), n, v);
 }
 template <typename R> __device__ __forceinline__ V<R> refract(V<R> i, V<R> n, R eta) {
     const R ndi = dot(n, i);
     const R k = R(1.0) - eta * eta * (R(1.0) - ndi * ndi);
-    if (k >= R(0)) return (eta * i) - ((eta * ndi + fast_sqrt(k)) * n);
+    if (k >= R(0)) return vfma(-(eta * ndi + fast_sqrt(k)), n, eta * i);
     return mk(R(0), R(0), R(0));
 }
 // dielectric.rs:13-19 (powi(5) = x * ((x*x)*(x*x)))
@@ -2555,7 +2570,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 dir = h.n + rs;
                 if (fabs(dir.x) < R(1e-8) && fabs(dir.y) < R(1e-8) && fabs(dir.z) < R(1e-8)) dir = h.n;
             } else {  // metal: draws even when fuzz = 0 (Q5)
-                dir = normalize(reflect(ray.d, h.n)) + m.param * rs;
+                dir = vfma(m.param, rs, normalize(reflect(ray.d, h.n)));
                 scattered = dot(dir, h.n) > R(0.0);
             }
             if (scattered) att = albedo(m, h);
@@ -2650,9 +2665,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ox = draw_taken<R>(g, R(-0.5), R(0.5));
                 oy = draw_taken<R>(g, R(-0.5), R(0.5));
             }
-            const V<R> point = (cam(0) + ((R)x + ox) * cam(1)) + ((R)y + oy) * cam(2);
+            const V<R> point = vfma((R)y + oy, cam(2), vfma((R)x + ox, cam(1), cam(0)));
             const V<R> disk = random_in_unit_disk<R>(g);
-            ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
+            ray.o = vfma(disk.y, cam(5), vfma(disk.x, cam(4), cam(3)));
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
             if (!EXACT || !(p.exact_all || p.exact_wbvh)) prep_ray<R, EXACT>(ray);  // 1/d: box tests only
@@ -2896,11 +2911,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ox = u01<R>(w.x) - R(0.5);
                 oy = u01<R>(w.y) - R(0.5);
             }
-            const V<R> point = (cam(0) + ((R)px + ox) * cam(1)) + ((R)py + oy) * cam(2);
+            const V<R> point = vfma((R)py + oy, cam(2), vfma((R)px + ox, cam(1), cam(0)));
             if (p.defocus) {
                 const uint4 wd = G::template block_at<R>(pixel_index(), cur, G::template defocus_step<R>());
                 const V<R> disk = unit_disk_inverse<R>(wd.x, wd.y);
-                ray.o = (cam(3) + disk.x * cam(4)) + disk.y * cam(5);
+                ray.o = vfma(disk.y, cam(5), vfma(disk.x, cam(4), cam(3)));
             } else {
                 ray.o = cam(3);  // zero disk: the draws would only scale zero vectors
             }

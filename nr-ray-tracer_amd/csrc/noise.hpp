@@ -41,6 +41,10 @@ struct FbmParams {
     double persistence = NOISE_DEFAULT_PERSISTENCE;
 };
 
+// Fbm::set_octaves: clamped to [1, NOISE_MAX_OCTAVES]
+inline uint32_t fbm_octaves(uint64_t octaves) {
+    return (uint32_t)(octaves < 1 ? 1 : (octaves > NOISE_MAX_OCTAVES ? NOISE_MAX_OCTAVES : octaves));
+}
 // f64::powi as LLVM lowers it (compiler-rt __powidf2: square-and-multiply).
 double powi_rt(double a, int b);
 // Fbm::calc_scale_factor

@@ -168,7 +168,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
                                     use_wbvh4(fs) ? wb4c : nullptr, fs.wbvh.root4, fs.wbvh.root,
                                     (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, 0u, nullptr, nullptr, 0u};
-        ds->wbvh_ok = fs.wbvh_ok;
+        ds->wbvh_ok = fs.wbvh_ok && fs.wbvh_f32_ok;  // (the f32 world-BVH modes)
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->planes = !fs.prims.empty();
         for (const DPrim<double>& pr : fs.prims) ds->planes &= pr.kind != PRIM_SPHERE;

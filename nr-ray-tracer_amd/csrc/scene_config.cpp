@@ -169,7 +169,7 @@ TexturePtr make_texture(const Value& cfg, const TextureMap& textures) {
         if (auto v = opt(*body, "persistence")) t->fbm.persistence = as_f64(*v, "persistence");
         uint64_t oct = 1;
         if (auto v = opt(*body, "octaves")) oct = as_usize(*v, "octaves");
-        t->fbm.octaves = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(oct, 1), NOISE_MAX_OCTAVES);
+        t->fbm.octaves = fbm_octaves(oct);
     } else {
         fail("unknown variant `" + kind + "` for TextureConfig");
     }

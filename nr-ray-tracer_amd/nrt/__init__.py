@@ -70,7 +70,7 @@ class _SceneStats(C.Structure):
                 ("materials", C.c_uint64), ("textures", C.c_uint64), ("texels", C.c_uint64), ("trees", C.c_uint32),
                 ("max_instance_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("world_prims", C.c_uint64),
                 ("coplanar_pairs", C.c_uint32), ("world_list_ok", C.c_uint32), ("exact_mode", C.c_uint32),
-                ("texel_bytes", C.c_uint32)]
+                ("reserved", C.c_uint32), ("texel_bytes", C.c_uint64)]
 
 
 PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
@@ -98,6 +98,9 @@ SIGNATURES = {
     "nrt_image_load": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                  C.c_size_t]),
     "nrt_texture_checker": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, C.c_double]),
+    "nrt_texture_noise": (C.c_int32, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_double, C.c_double,
+                                      C.c_double]),
+    "nrt_texture_marble": (C.c_int32, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_double]),
     "nrt_material_lambertian": (C.c_int32, [C.c_void_p, C.c_int32]),
     "nrt_material_metal": (C.c_int32, [C.c_void_p, C.c_double, C.c_int32]),
     "nrt_material_dielectric": (C.c_int32, [C.c_void_p, C.c_double]),
@@ -475,6 +478,19 @@ class Builder:
 
     def checker(self, even: int, odd: int, scale: float = 0.5) -> int:
         return _handle(lib().nrt_texture_checker(self._b, even, odd, scale))
+
+    def noise(self, seed: Optional[int] = None, octaves: Optional[int] = None, frequency: Optional[float] = None,
+              lacunarity: Optional[float] = None, persistence: Optional[float] = None) -> int:
+        """PerlinRidgedNoiseBuilder (noise.rs:30-101): None = the builder's default."""
+        fields = (seed, octaves, frequency, lacunarity, persistence)
+        set_ = sum(1 << k for k, v in enumerate(fields) if v is not None)
+        return _handle(lib().nrt_texture_noise(self._b, set_, seed or 0, octaves or 0, frequency or 0.0,
+                                               lacunarity or 0.0, persistence or 0.0))
+
+    def marble(self, seed: Optional[int] = None, frequency: Optional[float] = None) -> int:
+        """MarbleBuilder (marble.rs:24-60): None = the builder's default."""
+        set_ = (1 if seed is not None else 0) | (4 if frequency is not None else 0)
+        return _handle(lib().nrt_texture_marble(self._b, set_, seed or 0, frequency or 0.0))
 
     def lambertian(self, tex: int) -> int:
         return _handle(lib().nrt_material_lambertian(self._b, tex))

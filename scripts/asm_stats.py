@@ -16,7 +16,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FLAGS = ["-std=c++17", "-O3", "-fPIC", "-fno-fast-math", "-Wno-unused-function", "-x", "hip", "--offload-arch=gfx950",
-         "-ffp-contract=fast", "-mllvm", "-amdgpu-use-amdgpu-trackers", "--cuda-device-only", "-S",
+         os.environ.get("CONTRACT", "-ffp-contract=on"), "-mllvm", "-amdgpu-use-amdgpu-trackers", "--cuda-device-only", "-S",
          "-Rpass-analysis=kernel-resource-usage"]
 
 
@@ -27,7 +27,7 @@ def main():
     td = tempfile.mkdtemp()
     flags = list(FLAGS)
     if args and args[0] == "--exact":  # the exact kernels' contraction (kernels_exact.hip: none)
-        flags = [f if f != "-ffp-contract=fast" else "-ffp-contract=off" for f in flags]
+        flags = [f if f != os.environ.get("CONTRACT", "-ffp-contract=on") else "-ffp-contract=off" for f in flags]
         flags = [f for f in flags if f not in ("-mllvm", "-amdgpu-use-amdgpu-trackers")]
         args = args[1:]
     if args and args[0] == "--targs":

@@ -1,0 +1,71 @@
+"""`nrt-cli render` (the reference's `render` command, app/commands/render.rs:104-115, cli.rs:111-270).
+
+`--legacy-schema` is a switch (no value): it loads the index schema of scenes/triangles.toml
+(NRT_LOAD_LEGACY_SCHEMA), which the default loader rejects as the reference's does.  CPU: the
+load decision (without the switch the scene fails to load; with it the run gets past the load and
+stops only for want of a GPU).  GPU: the PFM the CLI writes equals the library's render of the same
+scene and camera, bit for bit.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import nrt
+from helpers import in_golden
+
+CLI = os.path.join(os.path.dirname(nrt.LIB_PATH), "nrt-cli")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def run(args, tmp_path):
+    env = dict(os.environ)
+    for k in list(env):
+        if k.startswith("NR_RT_CAMERA_"):
+            del env[k]
+    return subprocess.run([CLI, "render", *args], cwd=GOLDEN, capture_output=True, text=True, env=env, timeout=300)
+
+
+def read_pfm(path):
+    with open(path, "rb") as fh:
+        assert fh.readline().strip() == b"PF"
+        w, h = (int(x) for x in fh.readline().split())
+        assert float(fh.readline()) < 0  # little endian
+        data = np.frombuffer(fh.read(), dtype="<f4").reshape(h, w, 3)
+    return data[::-1]  # PFM rows run bottom to top
+
+
+def test_legacy_schema_refused_without_the_switch(tmp_path):
+    out = tmp_path / "t.pfm"
+    r = run(["scenes/triangles.toml", "-W", "16", "-H", "12", "-o", str(out), "-f"], tmp_path)
+    assert r.returncode != 0
+    assert "unknown flag" not in r.stderr
+    assert "GPUs" not in r.stderr and "visible" not in r.stderr, r.stderr  # it failed at the load
+
+
+def test_legacy_schema_switch_takes_no_value(tmp_path):
+    # the switch before the scene path: the path must stay the scene (round-3 ADVICE: the switch once
+    # swallowed it as its value)
+    out = tmp_path / "t.pfm"
+    r = run(["--legacy-schema", "scenes/triangles.toml", "-W", "16", "-H", "12", "-o", str(out), "-f"], tmp_path)
+    if nrt.device_count() < 1:
+        assert r.returncode != 0 and "visible" in r.stderr, r.stderr  # loaded; no GPU to render on
+    else:
+        assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args,precision,rng", [([], "f64", "chacha8"),
+                                                (["--precision", "f32", "--rng", "philox"], "f32", "philox")])
+def test_cli_pfm_equals_library_render(tmp_path, args, precision, rng):
+    out = tmp_path / "t.pfm"
+    r = run(["--legacy-schema", "scenes/triangles.toml", "-W", "40", "-H", "30", "--samples-per-pixel", "4",
+             "-o", str(out), "-f", *args], tmp_path)
+    assert r.returncode == 0, r.stderr
+    got = read_pfm(out)
+    with in_golden():
+        s = nrt.Scene.load("scenes/triangles.toml", nrt.CameraConfig(width=40, height=30, samples_per_pixel=4),
+                           legacy_schema=True)
+    want = s.render(precision=precision, rng=rng)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -95,12 +95,11 @@ def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace, rng
     """The hiprtc-built kernels (jit.hip: the world list's runs, or the world BVH's width and tie
     flag, as template arguments) are the generic kernel's code with the run loop unrolled or
     one traversal variant selected: same Philox draws and exact pixel sums, or the same ChaCha8
-    stream and f64 sum order (one lane per pixel).  Both contract a*b+c into FMAs where the backend sees fit (-ffp-contract=fast), and
-    the unrolled code fuses a few operations differently, so a path can part at the ulp level:
-    on the full C5 frame 3 of 1,048,576 pixels differ (scripts/jit_compare.py; with
-    -ffp-contract=on the frames are identical and the kernel 3 % slower), and the spheres
-    scene (dielectrics) parts on 0.2 % of its values at this size.  Bar:
-    >= 99 % of the values identical, channel means within 1 %."""
+    stream and f64 sum order (one lane per pixel).  Both builds contract only `a * b + c` written
+    as one expression (-ffp-contract=on) and fuse the vector helpers' products explicitly
+    (kernel.hpp fmad / vfma), so the unrolled code rounds as the generic code does and the frame
+    never depends on whether hiprtc is present (camera.rs:318-320: a pixel's value is a function
+    of its index alone).  Bar: bit-identical frames (the full C5 frame: scripts/jit_compare.py)."""
     s = load(scene, 40, 30, 64)
     if s.stats()["world_prims"] == 0 or (trace == "world-list" and not s.stats()["world_list_ok"]):
         pytest.skip("scene does not run this world mode")
@@ -113,14 +112,10 @@ def test_scene_specialised_kernel_matches_generic(monkeypatch, scene, trace, rng
     if (trace == "world-bvh" and scene.endswith("spheres.toml")) or (trace == "world-list" and rng == "chacha8"):
         # sphere scenes keep the generic BVH kernel, ChaCha8 the generic world-list kernel
         assert nrt.jit_stats()["launches"] == before["launches"]
-        np.testing.assert_array_equal(jit, generic)
-        return
-    assert nrt.jit_stats()["launches"] == before["launches"] + 1, "scene-specialised kernel not used"
+    else:
+        assert nrt.jit_stats()["launches"] == before["launches"] + 1, "scene-specialised kernel not used"
     assert np.isfinite(jit).all() and jit.max() > 0
-    same = np.mean(jit.view(np.uint32) == generic.view(np.uint32))
-    assert same >= 0.99, f"{same:.4f} of the values identical"
-    rel = np.abs(jit.reshape(-1, 3).mean(axis=0) / generic.reshape(-1, 3).mean(axis=0) - 1.0)
-    assert rel.max() < 0.01, rel
+    np.testing.assert_array_equal(jit.view(np.uint32), generic.view(np.uint32))
 
 
 def test_f32_philox_counter_limits():

@@ -47,6 +47,14 @@ def test_anchored_f32_spheres_follow_exact_paths(bounces, trace):
     assert mismatch(a, b) <= 0.01, mismatch(a, b)
 
 
+def test_far_anchored_sphere_keeps_the_exact_culling_walk():
+    """The far sphere bars only the f32 world-BVH kernels (their leaves hold the f32 test); the
+    tree is still built, so the reference-exact kernel keeps its world-BVH culling walk, which
+    tests every primitive it reaches in f64 (nrt.h NRT_EXACT_WORLD = 2)."""
+    assert scene(NEAR + FAR, 2).stats()["exact_mode"] == 2
+    assert scene(NEAR, 2).stats()["exact_mode"] == 2
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("bounces", [1, 2])
 def test_far_anchored_sphere_stays_f64(bounces):

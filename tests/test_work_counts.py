@@ -46,4 +46,14 @@ def test_bench_work_block():
     blk = bench.work_block(c5, 1000.0, "f32")
     assert blk["rays_per_s"] == pytest.approx(c5["rays_per_sample"] * 1e9, rel=1e-6)
     assert 0 < blk["valu_flop_frac"] < 1
-    assert bench.load_work(bench.DEFAULT_SCENE, 100, 100) is None
+    # another size of a counted scene takes that scene's per-sample counts and says so
+    other = bench.load_work(bench.DEFAULT_SCENE, 100, 100)
+    assert other["counted_at"] in ("512x512", "1024x1024") and other["scene"] == bench.DEFAULT_SCENE
+    assert bench.load_work("scenes/quads.toml", 100, 100) is None
+    # SURVEY §8(d) texel bytes at the bytes per texel as stored: 3-byte texels in 128-B lines of 40
+    assert bench.texel_payload_bytes({"texels": 40, "texel_bytes": 128}) == 3
+    assert bench.texel_payload_bytes({"texels": 32, "texel_bytes": 128}) == 4
+    assert bench.texel_payload_bytes({"texels": 4, "texel_bytes": 48}) == 12
+    assert bench.texel_payload_bytes({"texels": 0, "texel_bytes": 0}) == 0
+    c3 = bench.load_work("scenes/earth.toml", 1920, 1080)
+    assert c3["name"] == "C3" and c3["per_sample"]["texel_fetches"] > 0.2
