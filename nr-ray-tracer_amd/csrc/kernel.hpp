@@ -643,11 +643,56 @@ struct Rec {  // HitRecord (hitable.rs:14-22) of the closest hit, world space
 // computes (u, v) when a texture needs them (HitRecord::new_with_uv's sphere uv, sphere.rs:148-161):
 // the outward normal is n on the front face, -n on the back (n = -signum(d . outward) * outward).
 constexpr float UV_DEFERRED = -2.0f;
+// f32 acos / atan2 for the fast kernels' sphere uv: polynomials within 2.4e-7 / 1.4e-7 rad of the
+// true values (the libm f32 calls: 21 / 42 VALU, these 11 / 19).  A texel index floor(u * W) then
+// differs from the f64 one only within ~1e-4 texel of a texel edge (W = 2048), inside the f32
+// kernels' statistical tolerance; the f64 kernels keep libm's acos / atan2.
+//   acos: Abramowitz & Stegun 4.4.46, sqrt(1 - |x|) P7(|x|) (|err| <= 2e-8 in exact arithmetic),
+//         acos(-x) = pi - acos(x);
+//   atan2: a = min(|x|, |y|) / max(|x|, |y|), atan(a) = a P7(a^2) (least-squares fit on [0, 1]),
+//         then the octant.
+__device__ __forceinline__ float acos_f32(float x) {
+    const float a = fabsf(x);
+    float p = -0.0012624911f;
+    p = __builtin_fmaf(p, a, 0.0066700901f);
+    p = __builtin_fmaf(p, a, -0.0170881256f);
+    p = __builtin_fmaf(p, a, 0.0308918810f);
+    p = __builtin_fmaf(p, a, -0.0501743046f);
+    p = __builtin_fmaf(p, a, 0.0889789874f);
+    p = __builtin_fmaf(p, a, -0.2145988016f);
+    p = __builtin_fmaf(p, a, 1.5707963050f);
+    const float r = __builtin_amdgcn_sqrtf(1.0f - a) * p;
+    return x < 0.0f ? 3.14159265f - r : r;
+}
+__device__ __forceinline__ float atan2_f32(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float s = a * a;
+    float p = -0.0040731244f;
+    p = __builtin_fmaf(p, s, 0.0219459739f);
+    p = __builtin_fmaf(p, s, -0.0560623035f);
+    p = __builtin_fmaf(p, s, 0.0965619683f);
+    p = __builtin_fmaf(p, s, -0.1391578019f);
+    p = __builtin_fmaf(p, s, 0.1994850487f);
+    p = __builtin_fmaf(p, s, -0.3333010674f);
+    p = __builtin_fmaf(p, s, 0.9999994636f);
+    float r = a * p;
+    r = ay > ax ? 1.57079633f - r : r;
+    r = x < 0.0f ? 3.14159265f - r : r;
+    return __builtin_copysignf(r, y);
+}
 template <typename R>
 __device__ __forceinline__ void sphere_uv(const Rec<R>& h, R& u, R& v) {
     const V<R> geo = h.front ? h.n : -h.n;
-    const R theta = acos(-geo.y);
-    const R phi = atan2(-geo.z, geo.x) + R(M_PI);
+    R theta, phi;
+    if constexpr (sizeof(R) == 4) {
+        theta = acos_f32(-geo.y);
+        phi = atan2_f32(-geo.z, geo.x) + R(M_PI);
+    } else {
+        theta = acos(-geo.y);
+        phi = atan2(-geo.z, geo.x) + R(M_PI);
+    }
     u = phi * R(1.0 / (2.0 * M_PI));
     v = theta * R(1.0 / M_PI);
 }
@@ -2082,10 +2127,9 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
         if (q.kind == PRIM_SPHERE) {
             const V<R> center = ld3(q.n) + ray.time * ld3(q.A);
             outward = normalize(h.p - center);
-            const R theta = acos(-outward.y);
-            const R phi = atan2(-outward.z, outward.x) + R(M_PI);
-            h.u = phi * R(1.0 / (2.0 * M_PI));
-            h.v = theta * R(1.0 / M_PI);
+            h.front = true;  // (sphere_uv reads the outward normal as h.n on the front face)
+            h.n = outward;
+            sphere_uv(h, h.u, h.v);
         } else {
             h.u = dot(h.p, ld3(q.A)) - q.a0;
             h.v = dot(h.p, ld3(q.B)) - q.b0;
