@@ -954,7 +954,7 @@ struct WorldSig {
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
 // the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
 // plane-only scenes, and the unfiltered walk it falls back to).
-enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2 };
+enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2, EXACT_SIG_SLOTS = 3 };
 template <int MODE, int WIDTH, bool LSTACK = false>
 struct ExactSig {
     static constexpr uint32_t n = 0;
@@ -2014,12 +2014,57 @@ __device__ __forceinline__ bool trace_exact_slots_pf(const DSceneView<R>& sc, co
     return best_prim >= 0;
 }
 
+// Small scenes with spheres (at most EXACT_SLOTS_MAX slots of the culling tree, EXACT_SIG_SLOTS): the
+// reference test (Sphere::hit / Plane::hit in f64, sphere.rs:105-163, plane.rs:141-174) on every slot
+// in slot order, no walk, no boxes, no stack: the slot index is wave-uniform, so no lane waits for
+// another's walk, and the kernel variant carries no traversal code (the earth scene's f64 kernel
+// spilled 36 VGPRs with the walks compiled in).  The winner is the smallest t, ties to the higher
+// depth-first rank (object.rs:109-115), as the walks find it: the frame is the same bit for bit.
+template <typename R, int MAXD>
+__device__ __forceinline__ bool trace_exact_slots(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
+    static_assert(sizeof(R) == 8, "exact world mode is an f64-kernel mode");
+    R best_t = R(INFINITY);
+    uint32_t best_rank = 0;
+    int32_t best_prim = -1, best_inst = -1, cur_inst = -2;
+    Ray<R> oray = wray;
+    const uint32_t n = sc.n_wexact;
+    for (uint32_t k = 0; k < n; ++k) {
+        const DExactRef ref = sc.wexact[k];
+        if (ref.inst != cur_inst) {  // (wave-uniform: every lane switches together)
+            oray = wray;
+            if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
+            cur_inst = ref.inst;
+        }
+        const DPrim<R>& pr = sc.prims[ref.prim];
+        R t;
+        if (pr.kind == PRIM_SPHERE) {
+            t = sphere_t(pr, oray);
+        } else {
+            R alpha, beta;
+            V<R> point;
+            t = plane_t(pr, oray, alpha, beta, point);
+        }
+        if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
+            best_t = t;
+            best_rank = ref.rank;
+            best_prim = (int32_t)ref.prim;
+            best_inst = ref.inst;
+        }
+    }
+    hm.t = best_t;
+    hm.prim = (uint32_t)best_prim;
+    hm.depth = best_inst >= 0 ? 1 : 0;
+    hm.inst[0] = (uint32_t)best_inst;
+    return best_prim >= 0;
+}
+
 template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       STKP stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0,
                                       bool xthread = false) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
+    else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_SLOTS) return trace_exact_slots<R, MAXD>(sc, wray, hm);
     else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_SLOTS_PF) {
         static_assert(PF, "EXACT_SIG_SLOTS_PF is a KF_PLANES variant");
         return trace_exact_slots_pf<R, MAXD>(sc, wray, hm);
@@ -2144,10 +2189,18 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
         const V<R> center = ld3(pr.a) + ray.time * ld3(pr.b);
         h.p = vfma(t, ray.d, ray.o);
         outward = normalize(h.p - center);
-        const R theta = acos(-outward.y);
-        const R phi = atan2(-outward.z, outward.x) + R(M_PI);
-        h.u = phi / (R(2.0) * R(M_PI));
-        h.v = theta / R(M_PI);
+        // (u, v) only where a texture reads them (image, checker): the f64 acos / atan2 are the
+        // record's costliest part, and the earth scene's ground sphere is solid-coloured
+        const DMaterial& dm = sc.materials[pr.material];  // (a dielectric has no texture)
+        const uint32_t tk = dm.kind == MAT_DIELECTRIC ? (uint32_t)TEX_SOLID : sc.textures[dm.texture].kind;
+        h.u = R(0);
+        h.v = R(0);
+        if (tk == TEX_IMAGE || tk == TEX_CHECKER) {
+            const R theta = acos(-outward.y);
+            const R phi = atan2(-outward.z, outward.x) + R(M_PI);
+            h.u = phi / (R(2.0) * R(M_PI));
+            h.v = theta / R(M_PI);
+        }
     } else {  // plane.rs:156-159
         h.p = vfma(t, ray.d, ray.o);
         const V<R> ph = h.p - ld3(pr.a);
@@ -2460,8 +2513,27 @@ static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole 
 // Camera vector q of RenderParams: the f32 kernel takes the host-rounded copy
 // (kernel arguments stay in SGPRs), the f64 kernel the double.
 template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
-    if constexpr (sizeof(R) == 4) return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
-    else return ld3d<R>(d);
+    if constexpr (sizeof(R) == 4) {
+        return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
+    } else {
+        // f64: scalar loads from the kernel arguments at the use (the offset laundered, so the loads
+        // are not hoisted out of the loop): seven f64 vectors held live through the loop spilled the
+        // earth scene's exact kernel to scratch (42 registers' worth; the camera ray and the
+        // background are the only readers).  RenderParams is the kernel's first argument.
+        (void)p;
+        (void)d;
+        constexpr uint32_t off[7] = {
+            (uint32_t)__builtin_offsetof(RenderParams, top_left),       (uint32_t)__builtin_offsetof(RenderParams, pixel_delta_u),
+            (uint32_t)__builtin_offsetof(RenderParams, pixel_delta_v),  (uint32_t)__builtin_offsetof(RenderParams, look_from),
+            (uint32_t)__builtin_offsetof(RenderParams, defocus_disk_u), (uint32_t)__builtin_offsetof(RenderParams, defocus_disk_v),
+            (uint32_t)__builtin_offsetof(RenderParams, background)};
+        uint32_t o = off[q];
+        asm volatile("" : "+s"(o));
+        typedef const __attribute__((address_space(4))) unsigned char* KArg;
+        const KArg base = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
+        const __attribute__((address_space(4))) double* dp = (const __attribute__((address_space(4))) double*)(base + o);
+        return mk((R)dp[0], (R)dp[1], (R)dp[2]);
+    }
 }
 
 // Material of a hit, as the shading step needs it.

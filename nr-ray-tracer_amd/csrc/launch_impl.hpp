@@ -111,6 +111,17 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
         }
     }
     if constexpr (sizeof(R) == 8 && MAXD == 1 && G::exact_stream) {
+        if (!planes && !perlin && !p.counters && p.exact_wbvh && p.exact_slots && v.n_wexact <= dev::EXACT_SLOTS_MAX) {
+            // small scenes with spheres: the reference tests on every slot, no walk compiled in
+            // (the reference node array is never read: not staged)
+            DSceneView<R> vw = v;
+            vw.n_nodes = 0;
+            const uint32_t scene = lds_scene_bytes(vw, MAXD);
+            using XS = dev::ExactSig<dev::EXACT_SIG_SLOTS, 0>;
+            if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, 0, XS>(p, vw, ring + scene, stream);
+            else launch_variant<R, G, MAXD, EXACT, false, 0, XS>(p, vw, ring, stream);
+            return;
+        }
         if (planes && !perlin && !p.counters) {  // KF_PLANES: the 4-wave f64 variant
             if (p.exact_wbvh && p.exact_pf && !p.exact_all) {  // the prefiltered world walk only
                 // (the world walk never reads the reference node array: not staged, 2.4 KB of

@@ -26,7 +26,8 @@ def main():
     inc = ["-I" + os.path.join(pkg, "csrc"), "-I" + os.path.join(ROOT, "include")]
     td = tempfile.mkdtemp()
     flags = list(FLAGS)
-    if args and args[0] == "--exact":  # the exact kernels' contraction (kernels_exact.hip: none)
+    exact = bool(args) and args[0] == "--exact"
+    if exact:  # the exact kernels' contraction (kernels_exact.hip: none)
         flags = [f if f != os.environ.get("CONTRACT", "-ffp-contract=on") else "-ffp-contract=off" for f in flags]
         flags = [f for f in flags if f not in ("-mllvm", "-amdgpu-use-amdgpu-trackers")]
         args = args[1:]
@@ -41,7 +42,7 @@ def main():
         frag = ""
     else:
         frag = args.pop(0) if args and not args[0].startswith("-") else "PhiloxELi0ELb0ELb1ELi4EE"
-        src = os.path.join(pkg, "csrc", "kernels_fast.hip")
+        src = os.path.join(pkg, "csrc", "kernels_exact.hip" if exact else "kernels_fast.hip")
     out = os.path.join(td, "all.s")
     r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, *inc, src, "-o", out, *args], cwd=pkg, capture_output=True,
                        text=True)

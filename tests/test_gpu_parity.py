@@ -282,6 +282,7 @@ def test_fast_kernel_follows_exact_paths(scene, w, h, bounces, trace):
     ("scenes/utah-teapot-scene.json", 32, 24, 2),
     ("scenes/spheres.toml", 48, 27, 4),
     ("scenes/cube-scene.json", 40, 30, 4),   # touching coplanar cube faces: exact ties by rank
+    ("scenes/earth.toml", 48, 27, 2),        # spheres: the slots walk (EXACT_SIG_SLOTS) by default
 ])
 def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     """The three traversals of the reference-exact kernel (nrt.h nrt_exact_mode: the reference
@@ -292,8 +293,9 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     s = load(scene, w, h, spp)
     frames = {}
     # (all, world, prefilter, LDS stack, slots): the world walks run on the compact tree (16-bit stack
-    # entries, in scratch or, with NRT_EXACT_LSTACK, in LDS at 3 waves per SIMD); small plane-only
-    # scenes can prefilter every slot in order instead of walking (NRT_EXACT_SLOTS)
+    # entries, in scratch or, with NRT_EXACT_LSTACK, in LDS at 3 waves per SIMD); small scenes can
+    # visit every slot in order instead of walking (NRT_EXACT_SLOTS): plane-only scenes through the
+    # prefilter, scenes with spheres with the reference tests alone (EXACT_SIG_SLOTS)
     modes = {"bvh": ("0", "0", "0", "0", "0"), "all": ("1", "0", "0", "0", "0"), "world": ("0", "1", "0", "0", "0"),
              "world_pf": ("0", "1", "1", "0", "0"), "world_pf_lds_stack": ("0", "1", "1", "1", "0"),
              "world_pf_slots": ("0", "1", "1", "1", "1")}
