@@ -293,7 +293,13 @@ struct alignas(16) DMatFast {
 // RGB8T (default; NRT_TEX_RGB8=0 keeps RGBA8): the same bytes packed three per texel, tiles of 8 x 5 texels (120
 // bytes + 8 of padding, one 128-byte line): a line covers 40 texels instead of 32, at the cost of two
 // word loads and a byte align per lookup (tex_rgb8_byte; heights below 65536).
-enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1, TEXFMT_RGB8T = 2 };
+// PAL16 (default where it applies; NRT_TEX_PAL=0 keeps RGB8T): a 16-bit palette index per texel in
+// 8 x 8 tiles (one 128-byte line), then per horizontal band of 2^s rows a palette of at most 65536
+// RGBA8 words (band k's at 65536 k): images with few distinct colours per band (earth.jpg: 99 388 in
+// all, at most 62 033 per band of 256 rows; moon.jpg: 10 532) cost 2 bytes per texel instead of 3.2,
+// for a second, dependent load that mostly hits the L2 (the palettes are small).  The texture's `b`
+// holds the height | s << 16 (heights below 65536).
+enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1, TEXFMT_RGB8T = 2, TEXFMT_PAL16 = 3 };
 #if defined(__HIPCC_RTC__)
 #define NRT_HD __device__
 #elif defined(__HIPCC__)
@@ -308,6 +314,14 @@ NRT_HD inline uint64_t tex_tiled_index(uint32_t x, uint32_t y, uint32_t tiles_pe
 NRT_HD inline uint64_t tex_rgb8_byte(uint32_t x, uint32_t y, uint32_t tiles_per_row) {
     const uint32_t ty = (y * 52429u) >> 18, ly = y - 5u * ty;
     return ((uint64_t)ty * tiles_per_row + (x >> 3)) * 128u + (ly * 8u + (x & 7u)) * 3u;
+}
+// PAL16: 16-bit word index of texel (x, y) in the index array (two texels per 32-bit word), and
+// the words the index array takes
+NRT_HD inline uint64_t tex_pal_index(uint32_t x, uint32_t y, uint32_t tiles_per_row) {
+    return ((uint64_t)(y >> 3) * tiles_per_row + (x >> 3)) * 64u + (y & 7u) * 8u + (x & 7u);
+}
+NRT_HD inline uint64_t tex_pal_index_words(uint32_t w, uint32_t h) {
+    return (uint64_t)((w + 7u) >> 3) * ((h + 7u) >> 3) * 32u;
 }
 struct alignas(16) DTexture {
     uint32_t kind;

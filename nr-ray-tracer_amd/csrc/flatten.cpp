@@ -11,6 +11,7 @@
 #include <array>
 #include <deque>
 #include <map>
+#include <unordered_map>
 #include <stdexcept>
 
 #ifndef NRT_SPHERE_COST
@@ -72,6 +73,11 @@ struct Flattener {
                     return !(e && e[0] == '0');
                 }();
                 d.format = unorm8 ? TEXFMT_RGBA8 : TEXFMT_RGB32F;
+                static const bool pal_on = [] {  // knob NRT_TEX_PAL=0 (A/B runs): no palette format
+                    const char* e = std::getenv("NRT_TEX_PAL");
+                    return !(e && e[0] == '0');
+                }();
+                if (unorm8 && pal_on && t->height < 65536u && pal16_texture(*t, d)) break;
                 if (unorm8 && rgb8_on && t->height < 65536u) {  // 8 x 5 tiles of 3-byte texels (tex_rgb8_byte)
                     d.format = TEXFMT_RGB8T;
                     const uint32_t tw = (t->width + 7u) / 8u, th = (t->height + 4u) / 5u;
@@ -141,6 +147,54 @@ struct Flattener {
         out.textures.push_back(d);
         tex_ids[t.get()] = id;
         return id;
+    }
+
+    // PAL16 layout (device_scene.hpp) of a k / 255 image, if every band of 2^s rows (s as large as
+    // possible, at least 0) holds at most 65536 colours: index array, then the bands' palettes.
+    bool pal16_texture(const Texture& t, DTexture& d) {
+        const uint32_t W = t.width, H = t.height;
+        const std::vector<float>& px = *t.texels;
+        std::vector<uint32_t> rgb((size_t)W * H);
+        for (size_t i = 0; i < rgb.size(); ++i) {
+            uint32_t w = 0;
+            for (int c = 0; c < 3; ++c) w |= (uint32_t)std::nearbyint(px[3 * i + c] * 255.0f) << (8 * c);
+            rgb[i] = w;
+        }
+        uint32_t shift = 0;
+        while ((1u << shift) < H) ++shift;  // one band first
+        std::vector<std::vector<uint32_t>> pals;
+        std::vector<std::unordered_map<uint32_t, uint32_t>> maps;
+        for (;; --shift) {
+            const uint32_t bands = ((H - 1u) >> shift) + 1u;
+            pals.assign(bands, {});
+            maps.assign(bands, {});
+            bool ok = true;
+            for (uint32_t y = 0; y < H && ok; ++y) {
+                auto& m = maps[y >> shift];
+                auto& pal = pals[y >> shift];
+                for (uint32_t x = 0; x < W; ++x) {
+                    const uint32_t c = rgb[(size_t)y * W + x];
+                    if (m.emplace(c, (uint32_t)pal.size()).second) pal.push_back(c);
+                }
+                ok = pal.size() <= 65536u;
+            }
+            if (ok) break;
+            if (shift == 0 || bands >= 256u) return false;  // (too many colours per row band: RGB8T)
+        }
+        d.format = TEXFMT_PAL16;
+        d.b = H | (shift << 16);
+        const size_t base = out.texels.size();
+        const uint64_t iw = tex_pal_index_words(W, H);
+        out.texels.resize(base + iw + (size_t)pals.size() * 65536u, 0u);
+        uint16_t* idx = reinterpret_cast<uint16_t*>(out.texels.data() + base);
+        const uint32_t tw = (W + 7u) >> 3;
+        for (uint32_t y = 0; y < H; ++y)
+            for (uint32_t x = 0; x < W; ++x)
+                idx[tex_pal_index(x, y, tw)] = (uint16_t)maps[y >> shift].at(rgb[(size_t)y * W + x]);
+        for (size_t k = 0; k < pals.size(); ++k)
+            std::copy(pals[k].begin(), pals[k].end(), out.texels.begin() + (std::ptrdiff_t)(base + iw + k * 65536u));
+        // (the palettes' unused tail slots are never read; the allocation keeps each band at 65536 k)
+        return true;
     }
 
     uint32_t material(const MaterialPtr& m) {

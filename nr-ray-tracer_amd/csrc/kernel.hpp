@@ -1141,9 +1141,10 @@ __device__ __forceinline__ void wbvh_leaf(WbvhTrav& ts, const DSceneView<R>& sc,
 }
 
 // Traversal stacks.  f32 kernels: LDS, entry k of this lane at stack[k * BLOCK].  The exact
-// kernel's world-BVH mode: a private array (scratch), because its LDS holds the ChaCha8 ring
-// and the staged scene (an 8-entry LDS part, paid for by not staging the scene, measured
-// slower on every f64 config: C5 245 -> 323 ms, C4 400 -> 473 ms, C3 5.0 -> 6.0 ms).
+// kernel's world-BVH mode: the compact tree's 16-bit refs in LDS as well (ExactSig LSTACK, the
+// default since round 3: 3 waves per SIMD, no scratch traffic), or a private array (scratch:
+// NRT_EXACT_LSTACK=0; an 8-entry LDS part paid for by not staging the scene measured slower on
+// every f64 config: C5 245 -> 323 ms, C4 400 -> 473 ms, C3 5.0 -> 6.0 ms).
 struct PrivStack {
     int32_t e[WBVH_STACK + 1];
 };
@@ -1632,8 +1633,9 @@ __device__ __forceinline__ void xthread_walk(const DSceneView<R>& sc, const Ray<
 // is the smallest exact t, ties to the higher depth-first rank (object.rs:109-115), so the
 // visiting order does not matter.  The culling is conservative: the f32 boxes are rounded
 // outward and padded (1e-6 of the scene extent, far above the f32 slab error for origins
-// inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack is a
-// private array (PrivStack; the LDS holds the ChaCha8 ring and the staged scene).
+// inside the scene), and boxes are cut at the best exact t raised by 2^-20.  The stack: by default
+// the compact tree's 16-bit refs in LDS at 3 waves per SIMD (ExactSig LSTACK, NRT_EXACT_LSTACK),
+// else a private array (PrivStack / PrivStack16, scratch).
 // W: the culling walk fixed at compile time (ExactSig): XTHREAD_W the threaded tree, 4 / 2 the
 // stack walk of the 4-wide / binary tree; 0: chosen at run time (threaded when `thread`).
 constexpr int XTHREAD_W = 1;
@@ -2300,7 +2302,7 @@ __device__ __forceinline__ double perlin_texture(const uint32_t* texels, const D
 // product alone is 1 ulp off for 158 of them); explicit FMAs, so the exact kernel's
 // -ffp-contract=off build computes the same
 #ifndef NRT_TEX_FORMATS
-#define NRT_TEX_FORMATS 7  // image texel formats compiled in: 1 RGB32F, 2 RGBA8, 4 RGB8T (A/B via NRT_JIT_DEFS)
+#define NRT_TEX_FORMATS 15  // image texel formats compiled in: 1 RGB32F, 2 RGBA8, 4 RGB8T, 8 PAL16
 #endif
 __device__ __forceinline__ float unorm8(uint32_t k) {
     constexpr float r = 1.0f / 255.0f;
@@ -2328,12 +2330,21 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
         if (t.kind == TEX_IMAGE) {
             const R cu = u < R(0) ? R(0) : (u > R(1) ? R(1) : u);  // f64::clamp keeps NaN
             const R cv = v < R(0) ? R(0) : (v > R(1) ? R(1) : v);
+            const uint32_t th = t.format == TEXFMT_PAL16 ? (t.b & 0xFFFFu) : t.b;  // (PAL16: band shift above)
             const R fx = cu * (R)t.a;
-            const R fy = (R(1) - cv) * (R)t.b;
+            const R fy = (R(1) - cv) * (R)th;
             // `as u32` saturates (NaN -> 0); index W/H would panic in the
             // reference (Q12): clamped to the last texel here.
             uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
-            uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)t.b ? t.b - 1 : (uint32_t)fy);
+            uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)th ? th - 1 : (uint32_t)fy);
+            if ((NRT_TEX_FORMATS & 8) && t.format == TEXFMT_PAL16) {
+                // the texel's 16-bit palette index, then its band's palette word
+                const uint32_t* base = sc.texels + t.offset;
+                const uint64_t i = tex_pal_index(x, y, (t.a + 7u) >> 3);
+                const uint32_t pi = (base[i >> 1] >> ((uint32_t)(i & 1u) * 16u)) & 0xFFFFu;
+                const uint32_t w = base[tex_pal_index_words(t.a, th) + ((uint64_t)(y >> (t.b >> 16)) << 16) + pi];
+                return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
+            }
             if ((NRT_TEX_FORMATS & 4) && t.format == TEXFMT_RGB8T) {
                 // three bytes at a byte offset: the two words that hold them, aligned (v_alignbyte)
                 const uint64_t o = tex_rgb8_byte(x, y, (t.a + 7u) >> 3);
