@@ -181,17 +181,19 @@ def load_work(scene, w, h, spp=None):
     return same_scene
 
 
-# texel payload per format (device_scene.hpp TEXFMT_*): file images are 3 bytes per texel in 128-B
-# lines of 8 x 5 (3.2 B stored per texel with the line padding), RGBA8 words, or f32 RGB
-TEXEL_PAYLOAD = ((3.2, 3), (4.0, 4), (12.0, 12))
+# texel payload per format (device_scene.hpp TEXFMT_*), from the texel array's stored bytes per texel:
+# PAL16 = a 2-byte palette index per texel (+ per-band palettes: 2.0-2.8 B stored per texel; a lookup
+# reads the index from HBM and a palette word that stays in the L2), RGB8T = 3 bytes (3.2 stored with
+# the 128-B line padding), RGBA8 = 4, RGB32F = 12
+TEXEL_PAYLOAD = ((2.8, 2), (3.6, 3), (6.0, 4), (float("inf"), 12))
 
 
 def texel_payload_bytes(stats):
-    """Bytes per texel as stored (3 / 4 / 12), from the texel array's bytes per texel."""
+    """Bytes per texel fetch as stored (2 / 3 / 4 / 12), from the texel array's bytes per texel."""
     if not stats.get("texels"):
         return 0
     per = stats["texel_bytes"] / stats["texels"]
-    return min(TEXEL_PAYLOAD, key=lambda fp: abs(fp[0] - per))[1]
+    return next(b for lim, b in TEXEL_PAYLOAD if per < lim)
 
 
 def work_block(wc, msamples_per_s, precision):

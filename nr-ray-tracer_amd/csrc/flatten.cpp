@@ -73,10 +73,8 @@ struct Flattener {
                     return !(e && e[0] == '0');
                 }();
                 d.format = unorm8 ? TEXFMT_RGBA8 : TEXFMT_RGB32F;
-                static const bool pal_on = [] {  // knob NRT_TEX_PAL=0 (A/B runs): no palette format
-                    const char* e = std::getenv("NRT_TEX_PAL");
-                    return !(e && e[0] == '0');
-                }();
+                const char* pe = std::getenv("NRT_TEX_PAL");  // knob NRT_TEX_PAL=0 (A/B runs, tests): no palettes
+                const bool pal_on = !(pe && pe[0] == '0');
                 if (unorm8 && pal_on && t->height < 65536u && pal16_texture(*t, d)) break;
                 if (unorm8 && rgb8_on && t->height < 65536u) {  // 8 x 5 tiles of 3-byte texels (tex_rgb8_byte)
                     d.format = TEXFMT_RGB8T;

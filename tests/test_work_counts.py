@@ -52,6 +52,7 @@ def test_bench_work_block():
     assert bench.load_work("scenes/quads.toml", 100, 100) is None
     # SURVEY §8(d) texel bytes at the bytes per texel as stored: 3-byte texels in 128-B lines of 40
     assert bench.texel_payload_bytes({"texels": 40, "texel_bytes": 128}) == 3
+    assert bench.texel_payload_bytes({"texels": 4194304, "texel_bytes": 9437184}) == 2  # PAL16, earth.toml
     assert bench.texel_payload_bytes({"texels": 32, "texel_bytes": 128}) == 4
     assert bench.texel_payload_bytes({"texels": 4, "texel_bytes": 48}) == 12
     assert bench.texel_payload_bytes({"texels": 0, "texel_bytes": 0}) == 0
