@@ -55,6 +55,10 @@ constexpr int BLOCK = 256;
 #define NRT_SPHERE_REPROJ 1  // f32-tested spheres: hit points put back on the surface (make_record_world)
 #endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
+// ChaCha8 (persistent-lane) kernels' dynamic LDS before the stack and the staged scene: the ring,
+// then each lane's f64 pixel sums (kept in LDS, not registers: the earth scene's exact kernel spilled
+// them to scratch at every pixel)
+constexpr uint32_t CHACHA_LDS_BYTES = RING * BLOCK * 8u + 3u * BLOCK * 8u;
 
 template <typename R>
 struct V {
@@ -2590,7 +2594,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     };
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
-    const uint32_t acc_bytes = G::exact_stream ? 0u : philox_pool_bytes<MAXD>(p.wave_pixels);
+    const uint32_t acc_bytes = G::exact_stream ? 3u * BLOCK * (uint32_t)sizeof(double) : philox_pool_bytes<MAXD>(p.wave_pixels);
     // world-BVH stack (f32 kernels): the tree's bound + 1 entries (16-bit refs of the compact tree)
     using StackT = typename StackEntry<SIG::bvh == WBVH_COMPACT>::type;
     const uint32_t stack_bytes =
@@ -2728,21 +2732,21 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t i = p.pixel_begin + blockIdx.x * BLOCK + threadIdx.x;
         bool have = i < p.pixel_end;
         uint32_t x = 0, y = 0;
-        double ax = 0.0, ay = 0.0, az = 0.0;
+        double* const pacc = (double*)(lds + ring_bytes) + threadIdx.x;  // this lane's pixel sums, BLOCK apart
         uint32_t s = 0;  // next sample of the pixel
         auto start_pixel = [&]() {
             x = i % p.width;
             y = p.row_offset + (i / p.width) * p.row_stride;
             g.init((uint64_t)y * p.width + x, G::uses_lds ? (uint2*)lds + threadIdx.x : nullptr);  // stream (camera.rs:320-323)
-            ax = ay = az = 0.0;
+            pacc[0] = pacc[BLOCK] = pacc[2 * BLOCK] = 0.0;
             s = 0;
         };
         auto finish_pixel = [&]() {
             const double spp = (double)p.spp;
             float* o = p.out + 3ull * i;
-            o[0] = (float)(ax / spp);
-            o[1] = (float)(ay / spp);
-            o[2] = (float)(az / spp);
+            o[0] = (float)(pacc[0] / spp);
+            o[1] = (float)(pacc[BLOCK] / spp);
+            o[2] = (float)(pacc[2 * BLOCK] / spp);
         };
         const uint32_t dyn0 = p.pixel_begin + gridDim.x * BLOCK;  // first pixel handed out by the counters
         const uint32_t ndyn = p.pixel_end > dyn0 ? p.pixel_end - dyn0 : 0u;
@@ -2814,9 +2818,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const unsigned long long s1 = stamp();
             const bool cont = scatter && scatter_ray(h);
             if (!cont) {  // metal absorption adds contrib = 0
-                ax += (double)contrib.x;
-                ay += (double)contrib.y;
-                az += (double)contrib.z;
+                pacc[0] += (double)contrib.x;  // (the reference's f64 sum, in sample order)
+                pacc[BLOCK] += (double)contrib.y;
+                pacc[2 * BLOCK] += (double)contrib.z;
             }
             if constexpr (PROF) {
                 const unsigned long long s2 = stamp();
