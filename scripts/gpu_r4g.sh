@@ -13,3 +13,11 @@ timeout -k 10 700 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4h_ab_
 timeout -k 10 400 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4h_ab_c5.jsonl --lib B=nr-ray-tracer_amd/nrt/libnrt.so \
   --env w6="NRT_JIT_DEFS=" --env w8="NRT_JIT_DEFS=-DNRT_WORLD_LIST_WAVES=8" --env w7="NRT_JIT_DEFS=-DNRT_WORLD_LIST_WAVES=7" \
   --cfg c5="" 2>&1 | tail -4 || exit 1
+timeout -k 10 120 python scripts/shard_timing.py > gpurun_out/r4g_shard_tail1.json && cat gpurun_out/r4g_shard_tail1.json
+NRT_TAIL=0 timeout -k 10 120 python scripts/shard_timing.py > gpurun_out/r4g_shard_tail0.json && cat gpurun_out/r4g_shard_tail0.json
+timeout -k 10 500 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4g_ab_tail.jsonl --lib B=nr-ray-tracer_amd/nrt/libnrt.so \
+  --env t1="NRT_TAIL=1" --env t0="NRT_TAIL=0" --cfg c5="" --cfg c4="--scene scenes/utah-teapot-scene.json" --cfg c3="--scene scenes/earth.toml --width 1920 --height 1080 --spp 128" 2>&1 | tail -7
+timeout -k 10 900 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4g_ab_c4pp.jsonl --lib B=nr-ray-tracer_amd/nrt/libnrt.so \
+  --env base="NRT_JIT_DEFS=" --env pp6="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1" --env pp5="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_WBVH_WAVES=5" \
+  --env both5="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_NODE_PREFETCH=1 -DNRT_WBVH_WAVES=5" --env both4="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_NODE_PREFETCH=1 -DNRT_WBVH_WAVES=4" \
+  --cfg c4="--scene scenes/utah-teapot-scene.json" 2>&1 | tail -6
