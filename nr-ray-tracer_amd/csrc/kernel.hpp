@@ -2342,10 +2342,25 @@ __device__ __forceinline__ float unorm8(uint32_t k) {
 
 // Texture::get_color (solid_color.rs:35-43, textures/image.rs:31-40, checker.rs:76-89,
 // noise.rs:136-144, marble.rs:87-96); `p` = the world-space hit point
-template <typename R, bool PERLIN>
+template <typename R, bool PERLIN, bool PAL_ONLY = false>  // PAL_ONLY: solid colours and PAL16 images only (KF_TEXPAL)
 __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> p) {
-    for (int guard = 0; guard < 64; ++guard) {
+    for (int guard = 0; guard < (PAL_ONLY ? 1 : 64); ++guard) {
         const DTexture& t = sc.textures[tid];
+        if constexpr (PAL_ONLY) {  // (the same lookup as below, without the other kinds' and formats' code)
+            if (t.kind == TEX_SOLID) return ld3d<R>(t.color);
+            const R cu = u < R(0) ? R(0) : (u > R(1) ? R(1) : u);
+            const R cv = v < R(0) ? R(0) : (v > R(1) ? R(1) : v);
+            const uint32_t th = t.b & 0xFFFFu;
+            const R fx = cu * (R)t.a;
+            const R fy = (R(1) - cv) * (R)th;
+            const uint32_t x = !(fx > R(0)) ? 0u : (fx >= (R)t.a ? t.a - 1 : (uint32_t)fx);
+            const uint32_t y = !(fy > R(0)) ? 0u : (fy >= (R)th ? th - 1 : (uint32_t)fy);
+            const uint32_t* base = sc.texels + t.offset;
+            const uint64_t i = tex_pal_index(x, y, (t.a + 7u) >> 3);
+            const uint32_t pi = (base[i >> 1] >> ((uint32_t)(i & 1u) * 16u)) & 0xFFFFu;
+            const uint32_t w = base[tex_pal_index_words(t.a, th) + ((uint64_t)(y >> (t.b >> 16)) << 16) + pi];
+            return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
+        }
         if (t.kind == TEX_SOLID) return ld3d<R>(t.color);
         if (t.kind == TEX_NOISE || t.kind == TEX_MARBLE) {
             // (the host launches a PERLIN variant whenever the scene holds one of these)
@@ -2649,7 +2664,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             if (m.solid) return m.color;
             R u = h.u, v = h.v;
             if (MAXD <= 0 && u == R(UV_DEFERRED)) sphere_uv(h, u, v);
-            return tex_color<R, PERLIN>(sc, m.tex, u, v, h.p);
+            return tex_color<R, PERLIN, (KFLAGS & KF_TEXPAL) != 0>(sc, m.tex, u, v, h.p);
         }
     };
 

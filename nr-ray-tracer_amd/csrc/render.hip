@@ -54,6 +54,7 @@ struct DeviceScene {
     bool perlin = false;    // Noise / Marble textures present (KF_PERLIN kernel variants)
     bool planes = false;    // no spheres (the f64 kernel's KF_PLANES variant)
     bool flat = false;      // world list without spheres, solid colours only (KF_FLAT variants)
+    bool texpal = false;    // every texture a solid colour or a PAL16 image (KF_TEXPAL, scene-specialised kernels)
     const DPrimWorld<float>* wbvh_prims = nullptr;
     uint32_t n_wbvh_prims = 0;
     int wbvh_kinds = 0;  // WPRIMS_* of the world BVH's leaves (the scene-specialised kernel's BvhSig)
@@ -175,6 +176,9 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
         ds->planes = !fs.prims.empty();
         for (const DPrim<double>& pr : fs.prims) ds->planes &= pr.kind != PRIM_SPHERE;
         ds->flat = !ds->perlin;
+        ds->texpal = true;
+        for (const DTexture& t : fs.textures)
+            ds->texpal &= t.kind == TEX_SOLID || (t.kind == TEX_IMAGE && t.format == TEXFMT_PAL16);
         for (const DMatFast& m : fs.mats_fast) ds->flat &= m.solid != 0;
         // unit kinds from the runs (box / room units also hold header and empty face slots)
         for (uint32_t run : fs.wruns)
@@ -284,7 +288,8 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
             !ds->perlin && !q.counters) {
             std::string targs = std::string("float, nrt::dev::") + (rng == RNG_PHILOX ? "Philox, " : "ChaCha8, ") +
                                 std::to_string(maxd) + ", false, " +
-                                (staged ? "true, " : "false, ") + std::to_string(ds->flat ? dev::KF_FLAT : 0) + ", ";
+                                (staged ? "true, " : "false, ") +
+                                std::to_string(ds->flat ? dev::KF_FLAT : (ds->texpal ? dev::KF_TEXPAL : 0)) + ", ";
             if (maxd == MODE_WORLD_LIST) {
                 // ChaCha8 keeps the generic world-list kernel: its specialised build measured
                 // 1.85x slower on C5 (72 -> 133 ms), the Philox one 1.25x faster

@@ -20,8 +20,9 @@ constexpr uint32_t PHILOX2_MAX_BOUNCES = PHILOX2_STEPS - 2u;
 namespace dev {
 // Kernel variant flags (render_kernel's KFLAGS): KF_PROF = phase-profile stamps (diagnostics),
 // KF_PERLIN = the scene has Noise / Marble textures, KF_FLAT = world-mode scene without spheres
-// whose materials all have solid colours, KF_PLANES = f64 kernel, no spheres (kernel.hpp).
-constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8;
+// whose materials all have solid colours, KF_PLANES = f64 kernel, no spheres, KF_TEXPAL = every
+// texture is a solid colour or a PAL16 image (scene-specialised kernels only) (kernel.hpp).
+constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8, KF_TEXPAL = 16;
 }  // namespace dev
 
 struct RenderParams {

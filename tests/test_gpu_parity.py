@@ -88,6 +88,7 @@ def test_philox2x32_render_blocks(pixel0, sample):
 
 @pytest.mark.parametrize("scene,trace", [("scenes/cornell-box-scene.json", "world-list"),
                                          ("scenes/cube-scene.json", "world-list"), ("scenes/quads.toml", "world-list"),
+                                         ("scenes/earth.toml", "world-list"),  # PAL16 textures (KF_TEXPAL)
                                          ("scenes/utah-teapot-scene.json", "world-bvh"),
                                          ("scenes/spheres.toml", "world-bvh"), ("scenes/cornell-box-scene.json", "world-bvh")])
 @pytest.mark.parametrize("rng", ["philox", "chacha8"])
