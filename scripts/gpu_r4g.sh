@@ -21,3 +21,6 @@ timeout -k 10 900 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4g_ab_
   --env base="NRT_JIT_DEFS=" --env pp6="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1" --env pp5="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_WBVH_WAVES=5" \
   --env both5="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_NODE_PREFETCH=1 -DNRT_WBVH_WAVES=5" --env both4="NRT_JIT_DEFS=-DNRT_PRIM_PREFETCH=1 -DNRT_NODE_PREFETCH=1 -DNRT_WBVH_WAVES=4" \
   --cfg c4="--scene scenes/utah-teapot-scene.json" 2>&1 | tail -6
+timeout -k 10 600 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4g_ab_c5cam.jsonl --lib B=nr-ray-tracer_amd/nrt/libnrt.so \
+  --env base="NRT_JIT_DEFS=" --env cam7="NRT_JIT_DEFS=-DNRT_CAMF_AT_USE=1" --env cam8="NRT_JIT_DEFS=-DNRT_CAMF_AT_USE=1 -DNRT_WORLD_LIST_WAVES=8" \
+  --cfg c5="" --cfg c3="--scene scenes/earth.toml --width 1920 --height 1080 --spp 128" 2>&1 | tail -7
