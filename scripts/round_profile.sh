@@ -9,7 +9,9 @@ if [ "$half" = f32 ]; then
 bash scripts/profile.sh ${tag}_c5_f32_philox --steps 3 --warmup 1 && \
 bash scripts/profile.sh ${tag}_c4_f32_philox --scene scenes/utah-teapot-scene.json --steps 3 --warmup 1 && \
 bash scripts/profile.sh ${tag}_c3_f32_philox --scene scenes/earth.toml --width 1920 --height 1080 --spp 128 --steps 3 --warmup 1 && \
-bash scripts/profile.sh ${tag}_c2_f32_philox --width 512 --height 512 --spp 64 --steps 5 --warmup 1
+bash scripts/profile.sh ${tag}_c2_f32_philox --width 512 --height 512 --spp 64 --steps 5 --warmup 1 && \
+bash scripts/profile.sh ${tag}_c1_f32_philox --scene scenes/spheres.toml --width 400 --height 225 --spp 16 --steps 5 --warmup 1 && \
+bash scripts/profile.sh ${tag}_c1big_f32_philox --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 --steps 3 --warmup 1
 else
 bash scripts/profile.sh ${tag}_c5_f64_chacha8 --precision f64 --rng chacha8 --steps 2 --warmup 1 && \
 bash scripts/profile.sh ${tag}_c4_f64_chacha8 --scene scenes/utah-teapot-scene.json --precision f64 --rng chacha8 --steps 2 --warmup 1 && \
