@@ -377,16 +377,17 @@ def test_jit_require_refuses_the_generic_fallback(monkeypatch):
     assert nrt.jit_stats()["launches"] == before["launches"]  # the generic kernel rendered
 
 
-@pytest.mark.parametrize("defs", ["-DNRT_SLOTS_LIST=4", "-DNRT_SLOTS_BVH=8"])
+@pytest.mark.parametrize("defs", ["-DNRT_SLOTS_LIST=4", "-DNRT_SLOTS_BVH=8", "-DNRT_TEX_FORMATS=2"])
 def test_jit_defs_refuse_layout_macros(monkeypatch, defs):
-    """NRT_JIT_DEFS (an A/B tuning knob) may not change the Philox pool's LDS layout: the host sizes
-    the allocation from the library's own build (philox_pool_bytes), so a specialised kernel with
-    more slots would write past it (jit.hip refuses the render call instead)."""
-    s = load("scenes/cornell-box-scene.json", 32, 24, 2)
+    """NRT_JIT_DEFS (an A/B tuning knob) may not change the Philox pool's LDS layout or the texel
+    layout: the host sizes the allocations from the library's own build (philox_pool_bytes, the texel
+    formats it wrote), so a specialised kernel with more slots would write past its LDS, and one with
+    other texel formats would index the texels wrongly (jit.hip refuses the render call instead)."""
+    s = load("scenes/earth.toml" if "TEX" in defs else "scenes/cornell-box-scene.json", 32, 24, 2)
     monkeypatch.setenv("NRT_JIT_DEFS", defs)
     monkeypatch.setenv("NRT_JIT", "1")
-    with pytest.raises(nrt.NrtError, match="LDS layout"):
-        s.render(precision="f32", rng="philox", trace="world-list" if "LIST" in defs else "auto")
+    with pytest.raises(nrt.NrtError, match="layout"):
+        s.render(precision="f32", rng="philox", trace="world-list" if "LIST" in defs or "TEX" in defs else "auto")
 
 
 def test_exact_world_mode_far_camera(monkeypatch):
