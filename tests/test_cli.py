@@ -69,3 +69,22 @@ def test_cli_pfm_equals_library_render(tmp_path, args, precision, rng):
                            legacy_schema=True)
     want = s.render(precision=precision, rng=rng)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_cli_multi_gpu_rows_equal_single_gpu(tmp_path):
+    """`--gpus N` renders rows y = g (mod N) on device g from one host thread each and un-permutes
+    them (csrc/cli.cpp); every device runs its own scene-specialised kernel or, failing that, the
+    generic one, which renders the same bits, so the frame equals the one-GPU frame without
+    NRT_JIT=require."""
+    n = nrt.device_count()
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    outs = []
+    for g in (1, min(n, 4)):
+        out = tmp_path / f"g{g}.pfm"
+        r = run(["scenes/cornell-box-scene.json", "-W", "64", "-H", "48", "--samples-per-pixel", "8", "--precision",
+                 "f32", "--rng", "philox", "--gpus", str(g), "-o", str(out), "-f"], tmp_path)
+        assert r.returncode == 0, r.stderr
+        outs.append(read_pfm(out))
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
