@@ -361,12 +361,12 @@ def test_chacha8_persistent_lanes_grid_invariant(scene, w, h, spp, precision, mo
 
 
 def test_jit_require_refuses_the_generic_fallback(monkeypatch):
-    """NRT_JIT=require (jit.hip; bench.py sets it for N > 1): a scene-specialised build that fails
-    is an error of the render call, not a silent fallback to the generic kernel, whose f32 frame
-    can part from the specialised one's in the last bits; without it the generic kernel renders
-    and nrt_jit_stats counts the failure."""
+    """NRT_JIT=require (jit.hip): a scene-specialised build that fails is an error of the render call
+    instead of a fallback to the generic kernel (which renders the same bits, only slower: the knob
+    is for runs that must time the specialised kernel); without it the generic kernel renders and
+    nrt_jit_stats counts the failure."""
     s = load("scenes/cornell-box-scene.json", 32, 24, 2)
-    monkeypatch.setenv("NRT_JIT_DEFS", "-DNRT_GRAB=not_a_number")  # a build that cannot compile
+    monkeypatch.setenv("NRT_JIT_DEFS", "-DNRT_FETCH_AHEAD=not_a_number")  # a build that cannot compile
     monkeypatch.setenv("NRT_JIT", "require")
     with pytest.raises(nrt.NrtError, match="NRT_JIT=require"):
         s.render(precision="f32", rng="philox", trace="world-list")
