@@ -2564,20 +2564,8 @@ static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole 
 
 // Camera vector q of RenderParams: the f32 kernel takes the host-rounded copy
 // (kernel arguments stay in SGPRs), the f64 kernel the double.
-#ifndef NRT_CAMF_AT_USE
-#define NRT_CAMF_AT_USE 0  // f32: the camera vectors by scalar loads at their use (fewer SGPRs held)
-#endif
 template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
-    if constexpr (sizeof(R) == 4 && NRT_CAMF_AT_USE) {
-        (void)p;
-        (void)d;
-        uint32_t o = (uint32_t)__builtin_offsetof(RenderParams, camf) + 12u * (uint32_t)q;
-        asm volatile("" : "+s"(o));
-        typedef const __attribute__((address_space(4))) unsigned char* KArg;
-        const KArg base = (KArg)__builtin_amdgcn_kernarg_segment_ptr();
-        const __attribute__((address_space(4))) float* fp = (const __attribute__((address_space(4))) float*)(base + o);
-        return mk(fp[0], fp[1], fp[2]);
-    } else if constexpr (sizeof(R) == 4) {
+    if constexpr (sizeof(R) == 4) {
         return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
     } else {
         // f64: scalar loads from the kernel arguments at the use (the offset laundered, so the loads
