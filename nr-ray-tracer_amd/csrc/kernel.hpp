@@ -1081,9 +1081,6 @@ __device__ __forceinline__ T load16(const T* p) {  // whole record, 16-byte load
 #ifndef NRT_NODE_PREFETCH
 #define NRT_NODE_PREFETCH 0  // compact-tree if-if trips: load the next trip's node at the end of this one
 #endif
-#ifndef NRT_PRIM_PREFETCH
-#define NRT_PRIM_PREFETCH 0  // if-if trips: load the leaf cursor's next primitive at the end of a trip
-#endif
 struct WbvhTrav {
     int32_t node;
     int32_t leaf;  // parked leaf ref (< 0), WBVH_NO_LEAF when none
@@ -1092,7 +1089,6 @@ struct WbvhTrav {
     int32_t best;
     float ix, iy, iz, ox, oy, oz;  // 1/d and o/d: slab t = bound * inv - o * inv
     DBvh4cNode pre;  // NRT_NODE_PREFETCH: `node`'s record, loaded at the end of the previous trip
-    DPrimWorld<float> ppre;  // NRT_PRIM_PREFETCH: the leaf cursor's primitive, likewise
     __device__ __forceinline__ bool busy() const { return node != WBVH_DONE || leaf != WBVH_NO_LEAF; }
 };
 
@@ -1431,9 +1427,7 @@ __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>
     if (leaf_now) {  // (two primitives per trip measured C4 -6 %, round 2; 41.6 ms against 40.2, round 3)
         prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
         const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
-        DPrimWorld<float> q;
-        if constexpr (NRT_PRIM_PREFETCH) q = ts.ppre;
-        else q = load16(sc.wprims + first);
+        const DPrimWorld<float> q = load16(sc.wprims + first);
         const float t = world_prim_t<FLAT, TIE, PRIMS>(q, ray, ts.t_best);
         const bool ok = t >= 0.0f;
         ts.t_best = ok ? t : ts.t_best;
@@ -1454,9 +1448,6 @@ __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>
     }
     if constexpr (PREFETCH) {
         if (ts.node >= 0) ts.pre = load16(sc.wbvh4c + ts.node);
-    }
-    if constexpr (NRT_PRIM_PREFETCH) {
-        if (ts.leaf != WBVH_NO_LEAF) ts.ppre = load16(sc.wprims + ((~(uint32_t)ts.leaf) >> 3));
     }
 }
 // NRT_NODE_PREFETCH: the root's record for a query that begins (wbvh_begin)
@@ -3103,7 +3094,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             killed = false;
         };
 
-        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, {}, {}};
+        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, {}};
         auto begin = [&]() {  // world-BVH mode; depth cap / absorbed: no query (Q6)
             if constexpr (MAXD < 0) {
                 wbvh_begin(ts, (!killed && b < p.max_bounces) ? wbvh_root(gsc) : WBVH_DONE, ray);
