@@ -2499,6 +2499,9 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 
 // Philox sample pool: LDS slots per wave (a power of two; see the Philox branch of
 // render_kernel) and the pool's LDS bytes per workgroup for P pixels per group.
+#ifndef NRT_GRAB
+#define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
+#endif
 #ifndef NRT_PROBE_HEAD
 // 1: skip queue heads an agent-scope load shows empty before the atomic (saved C5 ~2 MB of HBM
 // writes, but the extra round trip before each fetch cost C3 earth 6.67 -> 7.32 ms): off
@@ -2963,27 +2966,18 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         constexpr uint32_t NS = philox_slots<MAXD>();
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
+        const uint32_t GS = P * p.spp;  // samples per group (host: < 2^32)
         // LDS per wave: NS slots x P pixel sums (3 x f64) and NS x P packed coordinates x | y << 16
         double* acc = (double*)(lds + ring_bytes) + wv * NS * P * 3u;
         uint32_t* slot_xy = (uint32_t*)(lds + ring_bytes + (BLOCK / 64) * NS * P * 3u * sizeof(double)) + wv * NS * P;
         constexpr uint32_t NO_GROUP = 0xFFFFFFFFu, PAD_XY = 0xFFFFFFFFu;
-        // per slot (wave-uniform): the group's first pixel, log2 of its pixels (P, or a tail group's
-        // 2^tail_log2), its finished samples
-        uint32_t gbase[NS], glog[NS], dones[NS];
+        uint32_t gids[NS], dones[NS];  // group held by each slot and its finished samples (wave-uniform)
 #pragma unroll
         for (uint32_t k = 0; k < NS; ++k) {
-            gbase[k] = NO_GROUP;
-            glog[k] = logP;
+            gids[k] = NO_GROUP;
             dones[k] = 0;
         }
-        auto gsamples = [&](uint32_t r) {  // samples of the group in slot r (host: < 2^32)
-            uint32_t lg = logP;
-#pragma unroll
-            for (uint32_t k = 0; k < NS; ++k) lg = k == r ? glog[k] : lg;
-            return p.spp << lg;
-        };
-        auto next_slot = [&](uint32_t r) { return NS == 2 ? r ^ 1u : (r + 1u) & (NS - 1u); };
-        uint32_t cs = 0, next = P * p.spp;          // claiming from slot cs at index next
+        uint32_t cs = 0, next = GS;                 // claiming from slot cs at index next
         bool ready = false;                         // slot (cs + 1) % NS holds a group not yet claimed from
         bool exhausted = false;                     // the queue is empty
         // Group distribution: per-XCD queue heads.  Head x hands out the x-th contiguous eighth
@@ -2992,49 +2986,51 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // image region: node, texel and framebuffer lines shared in the XCD's L1s and L2), and no
         // head is contended by more than one XCD's waves until the tail.  A device-scope atomic
         // executes at the memory side (one ~32-B HBM write each; with one per group they were
-        // 45 % of the C5 launch's HBM writes; several groups per atomic measured slower: C5 -5 %,
-        // guided runs C4 +50 %), and a head an agent-scope load already shows empty is skipped (a
-        // stale value only lags).  The XCD id only places work: never correctness.
-        // Tail groups: the last p.tail_groups groups of P pixels of every head are handed out as
-        // groups of 2^tail_log2 pixels, so the waves' last groups end sooner after the queues run
-        // dry (the launch ends with its slowest wave's last group).
+        // 45 % of the C5 launch's HBM writes): a wave takes NRT_GRAB consecutive groups per atomic
+        // (more per grab spreads the XCD's waves over a larger image region: guided runs of up
+        // to 25 groups cost C4 +50 %, C5 +12 %), and skips heads an agent-scope load already
+        // shows empty (a stale value only lags).  The XCD id only places work: never correctness.
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-        uint32_t qk = 0;  // heads found empty so far (wave-uniform)
-        auto fetch = [&](uint32_t r) {  // uniform: take the next group into (free) slot r
-            uint32_t base = NO_GROUP, lg = logP;
-            if (lane == 0) {
-                for (; qk < QUEUE_HEADS; ++qk) {
-                    const uint32_t x = (xcc + qk) & (QUEUE_HEADS - 1u);
-                    const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
-                    const uint32_t n = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS) - lo;
-                    const uint32_t nt = min(p.tail_groups, n), nb = n - nt;  // big groups, then the tail's
-                    const uint32_t ntot = nb + (nt << (logP - p.tail_log2));
-                    unsigned int* head = p.queue + x * QUEUE_STRIDE;
-                    if (ntot == 0 || (NRT_PROBE_HEAD && __hip_atomic_load(head, __ATOMIC_RELAXED,
-                                                                           __HIP_MEMORY_SCOPE_AGENT) >= ntot))
-                        continue;
-                    const uint32_t t = atomicAdd(head, 1u);
-                    if (t < ntot) {
-                        if (t < nb) {
-                            base = (lo + t) * P;
-                        } else {
-                            base = (lo + nb) * P + ((t - nb) << p.tail_log2);
-                            lg = p.tail_log2;
+        uint32_t qk = 0;              // heads found empty so far (wave-uniform)
+        uint32_t lcur = 0, lend = 0;  // groups of the last grab not yet taken (wave-uniform)
+        auto fetch = [&](uint32_t r) {              // uniform: take the next group into (free) slot r
+            uint32_t gid = 0xFFFFFFFFu;
+            if (NRT_GRAB > 1 && lcur < lend) {
+                gid = lcur++;
+            } else {
+                if (lane == 0) {
+                    for (; qk < QUEUE_HEADS; ++qk) {
+                        const uint32_t x = (xcc + qk) & (QUEUE_HEADS - 1u);
+                        const uint32_t lo = (uint32_t)((uint64_t)x * p.groups / QUEUE_HEADS);
+                        const uint32_t n = (uint32_t)((uint64_t)(x + 1u) * p.groups / QUEUE_HEADS) - lo;
+                        unsigned int* head = p.queue + x * QUEUE_STRIDE;
+                        if (n == 0 || (NRT_PROBE_HEAD && __hip_atomic_load(head, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT) >= n))
+                            continue;
+                        const uint32_t k = qk ? 1u : (uint32_t)NRT_GRAB;  // a steal takes one group
+                        const uint32_t t = atomicAdd(head, k);
+                        if (t < n) {
+                            gid = lo + t;
+                            lcur = gid + 1u;
+                            lend = lo + min(t + k, n);
+                            break;
                         }
-                        break;
                     }
                 }
+                gid = __builtin_amdgcn_readlane(gid, 0);
+                qk = __builtin_amdgcn_readlane(qk, 0);
+                if (NRT_GRAB > 1) {
+                    lcur = __builtin_amdgcn_readlane(lcur, 0);
+                    lend = __builtin_amdgcn_readlane(lend, 0);
+                }
             }
-            base = __builtin_amdgcn_readlane(base, 0);
-            lg = __builtin_amdgcn_readlane(lg, 0);
-            qk = __builtin_amdgcn_readlane(qk, 0);
-            exhausted = base == NO_GROUP;  // (plain stores and selects: the flags stay in registers)
+            exhausted = gid == 0xFFFFFFFFu;  // (plain stores and selects: the flags stay in registers)
             if (exhausted) return;
-            base += p.pixel_begin;
+            const uint32_t base = p.pixel_begin + gid * P;
             double* a = acc + r * P * 3u;
             uint32_t* xy = slot_xy + r * P;
-            for (uint32_t k = lane; k < (1u << lg); k += 64u) {
+            for (uint32_t k = lane; k < P; k += 64u) {
                 a[3 * k] = a[3 * k + 1] = a[3 * k + 2] = 0.0;
                 const uint32_t il = base + k;
                 xy[k] = il >= p.pixel_end ? PAD_XY
@@ -3044,20 +3040,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (uint32_t k = 0; k < NS; ++k) {
-                gbase[k] = k == r ? base : gbase[k];
-                glog[k] = k == r ? lg : glog[k];
+                gids[k] = k == r ? gid : gids[k];
                 dones[k] = k == r ? 0u : dones[k];
             }
             ready = true;
         };
-        auto flush = [&](uint32_t base, uint32_t lg, uint32_t r) {  // uniform: the group's last sample has finished
+        auto flush = [&](uint32_t gid, uint32_t r) {  // uniform: the group's last sample has finished
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             const double* a = acc + r * P * 3u;
             const double spp = (double)p.spp;
-            // the group's pixels are 3 x 2^lg contiguous floats in LDS and in the framebuffer:
+            const uint32_t base = p.pixel_begin + gid * P;
+            // the group's pixels are 3 x P contiguous floats in LDS and in the framebuffer:
             // one coalesced dword per lane (16-B stores cost the shading loop a spill)
-            const uint32_t nf = 3u * min(1u << lg, p.pixel_end - base);
+            const uint32_t nf = 3u * min(P, p.pixel_end - base);
             float* o = p.out + 3ull * base;
             for (uint32_t l = lane; l < nf; l += 64u) o[l] = (float)((a[l] * p.acc_unscale) / spp);
         };
@@ -3109,20 +3105,21 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             // fewer than a wave's worth of samples are left to claim.
 #pragma unroll
             for (uint32_t k = 0; k < NS; ++k) {
-                if (gbase[k] != NO_GROUP && dones[k] == (p.spp << glog[k])) {
-                    flush(gbase[k], glog[k], k);
-                    gbase[k] = NO_GROUP;
+                if (gids[k] != NO_GROUP && dones[k] == GS) {
+                    flush(gids[k], k);
+                    gids[k] = NO_GROUP;
                 }
             }
-            const uint32_t gs_cs = gsamples(cs);
-            if (!exhausted && !ready && gs_cs - next < NRT_FETCH_AHEAD) {
-                const uint32_t r = next_slot(cs);
+            if constexpr (NS == 2) {
+                if (!exhausted && !ready && GS - next < NRT_FETCH_AHEAD && (cs ? gids[0] : gids[1]) == NO_GROUP) fetch(cs ^ 1u);
+            } else if (!exhausted && !ready && GS - next < NRT_FETCH_AHEAD) {
+                const uint32_t r = (cs + 1u) & (NS - 1u);
                 bool free = false;
 #pragma unroll
-                for (uint32_t k = 0; k < NS; ++k) free |= k == r && gbase[k] == NO_GROUP;
+                for (uint32_t k = 0; k < NS; ++k) free |= k == r && gids[k] == NO_GROUP;
                 if (free) fetch(r);
             }
-            if (exhausted && !ready && gs_cs - next == 0u && __ballot(alive) == 0ull) break;
+            if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
             const unsigned long long t0 = stamp();
             HitMin<R, MAXD> hm;
             bool hit = false, sh, traced;
@@ -3188,32 +3185,24 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const bool want = ends || !alive;
             const uint64_t em = __ballot(want);
             const uint32_t nwant = (uint32_t)__popcll(em);
-            const uint32_t cs0 = cs, ns0 = next_slot(cs0);
-            const uint32_t gs0 = gsamples(cs0), gs1 = gsamples(ns0);
-            const uint32_t granted = min(nwant, (gs0 - next) + (ready ? gs1 : 0u));
+            const uint32_t granted = min(nwant, (GS - next) + (ready ? GS : 0u));
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(em >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)em, 0u));
             const uint32_t claim = next + rank;
+            const uint32_t cs0 = cs;
             next += granted;
-            if (next >= gs0 && ready) {
-                cs = ns0;
-                next -= gs0;
+            if (next >= GS && ready) {
+                cs = NS == 2 ? cs ^ 1u : (cs + 1u) & (NS - 1u);
+                next -= GS;
                 ready = false;
             }
             if (want) {
                 alive = rank < granted;
                 if (alive) {
-                    const bool second = claim >= gs0;
-                    slot = second ? ns0 : cs0;
-                    const uint32_t idx = second ? claim - gs0 : claim;
-                    uint32_t lg0 = logP, lg1 = logP;  // (wave-uniform selects)
-#pragma unroll
-                    for (uint32_t k = 0; k < NS; ++k) {
-                        lg0 = k == cs0 ? glog[k] : lg0;
-                        lg1 = k == ns0 ? glog[k] : lg1;
-                    }
-                    const uint32_t lg = second ? lg1 : lg0;
-                    j = idx & ((1u << lg) - 1u);
-                    cur = idx >> lg;
+                    const bool second = claim >= GS;
+                    slot = second ? (NS == 2 ? cs0 ^ 1u : (cs0 + 1u) & (NS - 1u)) : cs0;
+                    const uint32_t idx = second ? claim - GS : claim;
+                    j = idx & (P - 1u);
+                    cur = idx >> logP;
                     pxy = slot_xy[slot * P + j];
                 }
             }

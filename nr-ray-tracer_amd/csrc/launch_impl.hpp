@@ -62,24 +62,6 @@ static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&&
     p.wave_pixels_log2 = 0;
     while ((1u << p.wave_pixels_log2) < wp) ++p.wave_pixels_log2;
     p.groups = (npix + wp - 1) / wp;
-    // Tail groups: the last groups of every queue head in pieces of >= 256 samples (and at most half a
-    // group), about two per resident wave, at most a quarter of the head; NRT_TAIL=0 turns them off.
-    // The waves' last groups then end sooner once the queues run dry; which lane ran which sample
-    // never changes a pixel (exact sums), so the frame is the same.
-    p.tail_groups = 0;
-    p.tail_log2 = p.wave_pixels_log2;
-    const char* te = std::getenv("NRT_TAIL");
-    if (!(te && te[0] == '0') && wp > 1) {
-        uint32_t ql = 0;
-        while ((1u << ql) < wp / 2 && ((uint64_t)p.spp << ql) < 256) ++ql;
-        if ((1u << ql) < wp) {
-            const uint64_t per_head = (uint64_t)p.groups / QUEUE_HEADS;
-            const uint64_t small = 2 * waves_res / QUEUE_HEADS;  // pieces per head
-            const uint64_t big = (small << ql) / wp + 1;         // groups of wp pixels they come from
-            p.tail_log2 = ql;
-            p.tail_groups = (uint32_t)std::min<uint64_t>(big, per_head / 4);
-        }
-    }
     const uint64_t need = ((uint64_t)p.groups + dev::BLOCK / 64 - 1) / (dev::BLOCK / 64);
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min(waves_res / (dev::BLOCK / 64), need));
     launch(blocks, lds_fixed + ring_bytes(wp), p);

@@ -45,9 +45,6 @@ struct RenderParams {
     uint32_t wave_pixels, wave_pixels_log2;
     double acc_scale, acc_unscale;  // 2^k, 2^-k
     uint32_t groups;                // Philox: pixel groups (of wave_pixels) in this launch
-    // Philox: the last tail_groups groups of every queue head are handed out in pieces of
-    // 2^tail_log2 pixels (tail_log2 <= wave_pixels_log2; 0 groups: none), kernel.hpp fetch
-    uint32_t tail_groups, tail_log2;
     // Philox: QUEUE_HEADS group-queue heads, QUEUE_STRIDE words apart (device, zeroed
     // before the launch); head x hands out the x-th contiguous eighth of the groups
     // (kernel.hpp, Philox branch).  ChaCha8: word 0 counts the pixels handed out past the

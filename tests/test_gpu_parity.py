@@ -170,24 +170,6 @@ def test_philox_wave_size_is_bitwise_identical(monkeypatch, scene, precision, tr
         np.testing.assert_array_equal(s.render(precision=precision, rng="philox", trace=trace), full)
 
 
-@pytest.mark.parametrize("scene,trace", [("scenes/cornell-box-scene.json", "auto"),
-                                         ("scenes/utah-teapot-scene.json", "auto"), ("scenes/earth.toml", "auto")])
-def test_philox_tail_groups_are_bitwise_identical(monkeypatch, scene, trace):
-    """The last groups of every queue head go out in pieces of 2^tail_log2 pixels (launch_impl.hpp
-    philox_launch, kernel.hpp fetch) so the launch's last groups end sooner; every sample is still
-    rendered once with its own (pixel, sample) counter and summed exactly: the frame is the same with
-    and without them, for any group size."""
-    s = load(scene, 160, 96, 64, 12)
-    base = s.render(precision="f32", rng="philox", trace=trace)
-    assert np.isfinite(base).all() and base.max() > 0
-    for env in (("0", None), ("1", "8"), ("1", "64")):
-        monkeypatch.setenv("NRT_TAIL", env[0])
-        if env[1]:
-            monkeypatch.setenv("NRT_WAVE_PIXELS", env[1])
-        np.testing.assert_array_equal(s.render(precision="f32", rng="philox", trace=trace).view(np.uint32),
-                                      base.view(np.uint32))
-
-
 def test_row_interleave_is_bitwise_identical():
     # RNG keyed by pixel index: any row partition gives the same pixels (SURVEY §8e)
     scene, w, h, spp = "scenes/cornell-box-scene.json", 32, 21, 4
