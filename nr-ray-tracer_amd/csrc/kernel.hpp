@@ -1078,9 +1078,6 @@ __device__ __forceinline__ T load16(const T* p) {  // whole record, 16-byte load
 }
 
 // Traversal state of one lane's world-BVH query (kept in registers; the stack in LDS).
-#ifndef NRT_NODE_PREFETCH
-#define NRT_NODE_PREFETCH 0  // compact-tree if-if trips: load the next trip's node at the end of this one
-#endif
 struct WbvhTrav {
     int32_t node;
     int32_t leaf;  // parked leaf ref (< 0), WBVH_NO_LEAF when none
@@ -1088,7 +1085,6 @@ struct WbvhTrav {
     float t_best;
     int32_t best;
     float ix, iy, iz, ox, oy, oz;  // 1/d and o/d: slab t = bound * inv - o * inv
-    DBvh4cNode pre;  // NRT_NODE_PREFETCH: `node`'s record, loaded at the end of the previous trip
     __device__ __forceinline__ bool busy() const { return node != WBVH_DONE || leaf != WBVH_NO_LEAF; }
 };
 
@@ -1436,25 +1432,13 @@ __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>
     }
     // NRT_WBVH_UNIFIED: a lane holding both a leaf cursor and a node does both in one trip (a trip
     // runs both branches whenever the wave's lanes are mixed anyway); otherwise one or the other
-    constexpr bool PREFETCH = W == WBVH_COMPACT && NRT_NODE_PREFETCH;
     if ((NRT_WBVH_UNIFIED || !leaf_now) && ts.node >= 0) {
         prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
-        if constexpr (PREFETCH) wbvh4c_visit_nd(ts, ts.pre, stack);
-        else wbvh_visit_w<W>(ts, sc, stack);
+        wbvh_visit_w<W>(ts, sc, stack);
     }
     if (ts.leaf == WBVH_NO_LEAF && ts.node < 0 && ts.node != WBVH_DONE) {  // a leaf turned up: its cursor
         ts.leaf = ts.node;
         ts.node = wbvh_pop_w<W>(ts, stack);
-    }
-    if constexpr (PREFETCH) {
-        if (ts.node >= 0) ts.pre = load16(sc.wbvh4c + ts.node);
-    }
-}
-// NRT_NODE_PREFETCH: the root's record for a query that begins (wbvh_begin)
-template <class SIG, typename R>
-__device__ __forceinline__ void wbvh_prefetch_root(WbvhTrav& ts, const DSceneView<R>& sc) {
-    if constexpr (SIG::bvh == WBVH_COMPACT && NRT_NODE_PREFETCH) {
-        if (ts.node >= 0) ts.pre = load16(sc.wbvh4c + ts.node);
     }
 }
 template <typename R, int W, bool FLAT, class STKP>
@@ -3090,12 +3074,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             killed = false;
         };
 
-        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, {}};
+        WbvhTrav ts{WBVH_DONE, WBVH_NO_LEAF, 0u, INFINITY, -1, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         auto begin = [&]() {  // world-BVH mode; depth cap / absorbed: no query (Q6)
-            if constexpr (MAXD < 0) {
-                wbvh_begin(ts, (!killed && b < p.max_bounces) ? wbvh_root(gsc) : WBVH_DONE, ray);
-                wbvh_prefetch_root<SIG>(ts, gsc);
-            }
+            if constexpr (MAXD < 0) wbvh_begin(ts, (!killed && b < p.max_bounces) ? wbvh_root(gsc) : WBVH_DONE, ray);
         };
         const uint32_t wait_min = p.wave_wait ? p.wave_wait : 1u;
 
