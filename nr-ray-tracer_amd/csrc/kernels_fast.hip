@@ -25,13 +25,9 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
                      uint32_t rng, uint32_t stack_entry, hipStream_t stream) {
     const hipFunction_t fn = (hipFunction_t)fnp;
     auto resident = [&](uint32_t lds) {
-        int per_cu = 0, dev_id = 0, cus = 0;
-        if (hipGetDevice(&dev_id) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
-            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, dev::BLOCK, lds) != hipSuccess ||
-            per_cu <= 0 || cus <= 0)
-            throw std::runtime_error("occupancy query failed for the scene-specialised kernel");
-        return (uint64_t)per_cu * (uint64_t)cus;
+        return cached_resident((const void*)fn, lds, [&](int* per_cu) {
+            return hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, fn, dev::BLOCK, lds) == hipSuccess;
+        });
     };
     auto launch = [&](uint32_t blocks, uint32_t lds, const RenderParams& p) {
         RenderParams pp = p;

@@ -3,7 +3,10 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <stdexcept>
+#include <tuple>
 
 #include "kernel.hpp"
 #include "launch.hpp"
@@ -19,16 +22,35 @@ inline uint64_t chacha_grid_cap() {
     return v > 0 ? (uint64_t)v : ~0ull;
 }
 
-// Blocks the device keeps resident for one kernel variant.
+// Blocks the device keeps resident for a kernel (static or a module function) with `lds_bytes` of
+// dynamic LDS, cached per (device, kernel, LDS): the occupancy queries cost the host tens of
+// microseconds per launch, which a short launch (a row shard at N = 8) waits for on the GPU.
+template <class Query>
+static uint64_t cached_resident(const void* kernel, uint32_t lds_bytes, Query&& query) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void*, uint32_t>, uint64_t> cache;
+    int dev_id = 0;
+    if (hipGetDevice(&dev_id) != hipSuccess) throw std::runtime_error("hipGetDevice failed");
+    const auto key = std::make_tuple(dev_id, kernel, lds_bytes);
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    int per_cu = 0, cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
+        !query(&per_cu) || per_cu <= 0 || cus <= 0)
+        throw std::runtime_error("occupancy query failed for the render kernel");
+    const uint64_t n = (uint64_t)per_cu * (uint64_t)cus;
+    std::lock_guard<std::mutex> lock(mu);
+    cache[key] = n;
+    return n;
+}
 template <typename K>
 static uint64_t resident_blocks(K kernel, uint32_t lds_bytes) {
-    int per_cu = 0, dev_id = 0, cus = 0;
-    if (hipGetDevice(&dev_id) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev_id) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, dev::BLOCK, lds_bytes) != hipSuccess ||
-        per_cu <= 0 || cus <= 0)
-        throw std::runtime_error("occupancy query failed for the render kernel");
-    return (uint64_t)per_cu * (uint64_t)cus;
+    return cached_resident((const void*)kernel, lds_bytes, [&](int* per_cu) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kernel, dev::BLOCK, lds_bytes) == hipSuccess;
+    });
 }
 
 // Philox: persistent waves (as many blocks as stay resident, capped by the group
