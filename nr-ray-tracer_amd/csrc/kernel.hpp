@@ -2768,28 +2768,40 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
         uint32_t qk = 0;  // counters found exhausted (wave-uniform; QUEUE_HEADS: no pixel left)
+        // The wave's reservoir (uniform): pixels [rb, rb + rn) claimed but not yet started.  Lanes
+        // free up one at a time, so a claim of only the lanes asking cost one counter atomic per
+        // pixel and a wait on its return; a claim takes at least p.exact_claim pixels (the host's
+        // pick by spp, render.hip) and later asks are served from the reservoir.
+        uint32_t rb = 0, rn = 0;
         auto next_pixel = [&](bool need) -> bool {  // uniform; true: this lane got a pixel
             const uint64_t m = __ballot(need);
-            if (m == 0ull || qk >= QUEUE_HEADS) return false;
+            if (m == 0ull) return false;
             const uint32_t cnt = (uint32_t)__popcll(m);
-            uint32_t base = 0, grant = 0;
-            if (leader()) {
-                for (; qk < QUEUE_HEADS; ++qk) {
-                    const uint32_t xh = (xcc + qk) & (QUEUE_HEADS - 1u);
-                    const uint32_t lo = (uint32_t)((uint64_t)xh * ndyn / QUEUE_HEADS);
-                    const uint32_t n = (uint32_t)((uint64_t)(xh + 1u) * ndyn / QUEUE_HEADS) - lo;
-                    if (n == 0) continue;
-                    const uint32_t t = atomicAdd(p.queue + xh * QUEUE_STRIDE, cnt);
-                    if (t < n) {
-                        base = lo + t;
-                        grant = min(cnt, n - t);
-                        break;
+            if (rn == 0 && qk < QUEUE_HEADS) {
+                const uint32_t want = max(cnt, p.exact_claim);
+                uint32_t base = 0, got = 0;
+                if (leader()) {
+                    for (; qk < QUEUE_HEADS; ++qk) {
+                        const uint32_t xh = (xcc + qk) & (QUEUE_HEADS - 1u);
+                        const uint32_t lo = (uint32_t)((uint64_t)xh * ndyn / QUEUE_HEADS);
+                        const uint32_t n = (uint32_t)((uint64_t)(xh + 1u) * ndyn / QUEUE_HEADS) - lo;
+                        if (n == 0) continue;
+                        const uint32_t t = atomicAdd(p.queue + xh * QUEUE_STRIDE, want);
+                        if (t < n) {
+                            base = lo + t;
+                            got = min(want, n - t);
+                            break;
+                        }
                     }
                 }
+                rb = __builtin_amdgcn_readfirstlane(base);
+                rn = __builtin_amdgcn_readfirstlane(got);
+                qk = __builtin_amdgcn_readfirstlane(qk);
             }
-            base = __builtin_amdgcn_readfirstlane(base);
-            grant = __builtin_amdgcn_readfirstlane(grant);
-            qk = __builtin_amdgcn_readfirstlane(qk);
+            if (rn == 0) return false;
+            const uint32_t base = rb, grant = min(cnt, rn);
+            rb += grant;
+            rn -= grant;
             if (!need) return false;
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             if (rank >= grant) return false;  // (the next round asks again)

@@ -256,6 +256,10 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     RenderParams q = p;
     if (q.wave_wait == 0)  // if-if trips (KF_FLAT world BVH) shade at 24 finished lanes (C4 34.6 -> 34.3 ms),
         q.wave_wait = ds->flat ? 24u : 32u;  // the sphere / texture variant at 32 (spheres.toml 1080p: 31.06 ms at 24, 30.71 at 32)
+    // Persistent lanes: claims of 128/spp pixels (1..8).  Short pixels end often, and a claim per
+    // finished pixel stalls the wave on the atomic's return (earth f64 spp 16: 6.26 -> 5.87 ms at
+    // 8); long ones hold the reservoir's pixels into the tail (C4 f64 spp 256: 191 -> 201 ms at 8).
+    if (q.exact_claim == 0) q.exact_claim = std::min(8u, std::max(1u, 128u / std::max(1u, q.spp)));
     {  // Philox: group queue heads; ChaCha8: the pixel counter of the persistent lanes (head 0)
         const size_t qwords = (size_t)QUEUE_HEADS * QUEUE_STRIDE;
         q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;

@@ -81,6 +81,9 @@ struct RenderParams {
     // Exact world mode with the prefilter, at most EXACT_SLOTS_MAX slots: the prefilter over every
     // slot in order (scalar loads, no walk) instead of the culling walk (EXACT_SIG_SLOTS_PF).
     uint32_t exact_slots;
+    // Persistent lanes (ChaCha8): fewest pixels a wave claims per counter atomic; the rest wait in
+    // the wave's reservoir (kernel.hpp next_pixel).  0: the host picks (render.hip).
+    uint32_t exact_claim;
     float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
 };
 
