@@ -2,6 +2,8 @@
 row shard (rows y = 0 mod N) for N = 1, 2, 4, 8, against 1/N of the full frame.
 
 usage: python scripts/shard_timing.py [scene] [W H spp] [N,N,...]
+SHARD_MAX_BOUNCES=B overrides the scene's bounce cap (diagnostic: how much of the fixed per-launch
+loss is the longest paths' serial bounces).
 Each N is timed two ways: `shard_ms` brackets one launch with events after a synchronize (the host's
 launch work, occupancy queries and hipModuleLaunchKernel, counts when the GPU waits for it), and
 `shard_ms_queued` the same launch enqueued behind a previous one, so the GPU is still busy while the
@@ -20,7 +22,8 @@ import nrt  # noqa: E402
 scene = sys.argv[1] if len(sys.argv) > 1 else "scenes/cornell-box-scene.json"
 W, H, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1024, 1024, 256)
 os.chdir(os.path.join(ROOT, "tests", "golden"))
-s = nrt.Scene.load(scene, nrt.CameraConfig(width=W, height=H, samples_per_pixel=spp))
+mb = int(os.environ["SHARD_MAX_BOUNCES"]) if os.environ.get("SHARD_MAX_BOUNCES") else None
+s = nrt.Scene.load(scene, nrt.CameraConfig(width=W, height=H, samples_per_pixel=spp, ray_max_bounces=mb))
 s.upload(0)
 buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
 stream = torch.cuda.current_stream()
@@ -53,5 +56,5 @@ base, baseq = res[ns[0]] * ns[0], resq[ns[0]] * ns[0]
 out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(base / (n * t), 4),
                   "shard_ms_queued": round(resq[n], 3), "efficiency_queued": round(baseq / (n * resq[n]), 4)}
        for n, t in res.items()}
-out["env"] = {k: v for k, v in os.environ.items() if k.startswith("NRT_")}
+out["env"] = {k: v for k, v in os.environ.items() if k.startswith(("NRT_", "SHARD_"))}
 print(json.dumps(out))
