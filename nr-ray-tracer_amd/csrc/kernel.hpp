@@ -59,6 +59,16 @@ constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in 
 // then each lane's f64 pixel sums (kept in LDS, not registers: the earth scene's exact kernel spilled
 // them to scratch at every pixel)
 constexpr uint32_t CHACHA_LDS_BYTES = RING * BLOCK * 8u + 3u * BLOCK * 8u;
+// Persistent lanes with pixel claims of 2..8 (spp <= 64, render.hip): each wave stages the finished
+// pixels of up to STG_SLOTS claims in LDS (3 floats per pixel, then per claim its pixels left, first
+// pixel and size) and writes a claim out as one coalesced run once its last pixel is done, instead of
+// 12 scattered bytes per pixel (each costing a partial-line write-back: earth f64 87 -> 66 MB).
+constexpr uint32_t STG_SLOTS = 8, STG_PX = 8, NO_STG = 0xFFFFFFFFu;
+constexpr uint32_t STG_WAVE_WORDS = STG_SLOTS * (STG_PX * 3u + 3u);
+constexpr uint32_t STG_LDS_BYTES = (BLOCK / 64u) * STG_WAVE_WORDS * 4u;
+__host__ __device__ inline uint32_t chacha_lds_bytes(uint32_t exact_claim) {
+    return CHACHA_LDS_BYTES + (exact_claim > 1u ? STG_LDS_BYTES : 0u);
+}
 
 template <typename R>
 struct V {
@@ -2609,7 +2619,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     };
     // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
-    const uint32_t acc_bytes = G::exact_stream ? 3u * BLOCK * (uint32_t)sizeof(double) : philox_pool_bytes<MAXD>(p.wave_pixels);
+    const uint32_t acc_bytes = G::exact_stream ? chacha_lds_bytes(p.exact_claim) - ring_bytes
+                                               : philox_pool_bytes<MAXD>(p.wave_pixels);
     // world-BVH stack (f32 kernels): the tree's bound + 1 entries (16-bit refs of the compact tree)
     using StackT = typename StackEntry<SIG::bvh == WBVH_COMPACT>::type;
     const uint32_t stack_bytes =
@@ -2756,14 +2767,55 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             pacc[0] = pacc[BLOCK] = pacc[2 * BLOCK] = 0.0;
             s = 0;
         };
+        // claim staging (STG_SLOTS): this wave's slots, each STG_PX x 3 floats then (left, first, size)
+        const bool staging = p.exact_claim > 1u;  // (host: the LDS holds the slots only then)
+        uint32_t* const stg = (uint32_t*)(lds + ring_bytes + 3u * BLOCK * (uint32_t)sizeof(double)) + wv * STG_WAVE_WORDS;
+        auto stg_meta = [&](uint32_t slot) { return stg + STG_SLOTS * STG_PX * 3u + slot * 3u; };
+        uint32_t stg_free = (1u << STG_SLOTS) - 1u;  // uniform: free slots
+        uint32_t rslot = NO_STG, rfirst = 0;        // uniform: slot and first pixel of the reservoir's claim
+        uint32_t stag = NO_STG;                     // this lane's pixel: slot << 8 | its place in the claim
+        uint32_t ended = NO_STG;                    // slot whose last pixel this lane just finished
         auto finish_pixel = [&]() {
             const double spp = (double)p.spp;
-            float* o = p.out + 3ull * i;
-            o[0] = (float)(pacc[0] / spp);
-            o[1] = (float)(pacc[BLOCK] / spp);
-            o[2] = (float)(pacc[2 * BLOCK] / spp);
+            const float c0 = (float)(pacc[0] / spp), c1 = (float)(pacc[BLOCK] / spp), c2 = (float)(pacc[2 * BLOCK] / spp);
+            if (stag != NO_STG) {
+                const uint32_t slot = stag >> 8;
+                float* d = (float*)stg + slot * (STG_PX * 3u) + (stag & 0xFFu) * 3u;
+                d[0] = c0;
+                d[1] = c1;
+                d[2] = c2;
+                if (atomicSub(stg_meta(slot), 1u) == 1u) ended = slot;  // the claim's last pixel
+                stag = NO_STG;
+            } else {
+                float* o = p.out + 3ull * i;
+                o[0] = c0;
+                o[1] = c1;
+                o[2] = c2;
+            }
         };
         const uint32_t dyn0 = p.pixel_begin + gridDim.x * BLOCK;  // first pixel handed out by the counters
+        // uniform, after the lanes' finish_pixel: write out the claims whose last pixel ended
+        auto flush_claims = [&]() {
+            if (!staging) return;
+            uint64_t fm = __ballot(ended != NO_STG);
+            if (fm == 0ull) return;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t lane = threadIdx.x & 63u;
+            while (fm) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(fm);
+                fm &= fm - 1ull;
+                const uint32_t slot = __builtin_amdgcn_readlane(ended, l);
+                const uint32_t first = stg_meta(slot)[1], nf = 3u * stg_meta(slot)[2];
+                const float* d = (const float*)stg + slot * (STG_PX * 3u);
+                float* o = p.out + 3ull * (dyn0 + first);
+                for (uint32_t k = lane; k < nf; k += 64u) o[k] = d[k];
+                stg_free |= 1u << slot;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            ended = NO_STG;
+        };
         const uint32_t ndyn = p.pixel_end > dyn0 ? p.pixel_end - dyn0 : 0u;
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
@@ -2797,6 +2849,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 rb = __builtin_amdgcn_readfirstlane(base);
                 rn = __builtin_amdgcn_readfirstlane(got);
                 qk = __builtin_amdgcn_readfirstlane(qk);
+                rslot = NO_STG;
+                if (staging && rn != 0 && rn <= STG_PX && stg_free != 0u) {  // a staging slot for the claim
+                    rslot = (uint32_t)__builtin_ctz(stg_free);
+                    rfirst = rb;
+                    stg_free &= ~(1u << rslot);
+                    if ((threadIdx.x & 63u) == 0u) {
+                        uint32_t* mt = stg_meta(rslot);
+                        mt[0] = rn;
+                        mt[1] = rb;
+                        mt[2] = rn;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
             if (rn == 0) return false;
             const uint32_t base = rb, grant = min(cnt, rn);
@@ -2806,6 +2872,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             if (rank >= grant) return false;  // (the next round asks again)
             i = dyn0 + base + rank;
+            stag = rslot == NO_STG ? NO_STG : (rslot << 8) | (base + rank - rfirst);
             have = true;
             start_pixel();
             return true;
@@ -2903,6 +2970,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     finish_pixel();
                     have = false;
                 }
+                flush_claims();
                 if (next_pixel(!have)) {
                     active = camera_ray();
                     begin();
@@ -2916,6 +2984,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     finish_pixel();
                     have = false;
                 }
+                flush_claims();
                 next_pixel(!have);
                 if (__ballot(have) == 0ull) break;  // (no lane holds a pixel: the counters are exhausted)
                 if (!have) continue;

@@ -39,7 +39,7 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
     const uint32_t stack = maxd == MODE_WORLD_BVH ? (v.wbvh_stack + 1u) * dev::BLOCK * stack_entry : 0u;
     if (rng == RNG_CHACHA8) {  // persistent lanes (launch_variant): ring + stack below the staged scene
         const uint32_t npix = p0.pixel_end - p0.pixel_begin;
-        const uint32_t lds = lds_fixed + dev::CHACHA_LDS_BYTES + stack;
+        const uint32_t lds = lds_fixed + dev::chacha_lds_bytes(p0.exact_claim) + stack;
         const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
         launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({need, resident(lds), chacha_grid_cap()})), lds, p0);
         return;

@@ -112,7 +112,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                        bool flat = false, bool planes = false) {
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
-    const uint32_t ring = (G::uses_lds ? dev::CHACHA_LDS_BYTES : 0) +
+    const uint32_t ring = (G::uses_lds ? dev::chacha_lds_bytes(p.exact_claim) : 0) +
                           (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v, MAXD);
     using dev::KF_FLAT;
