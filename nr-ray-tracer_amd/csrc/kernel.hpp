@@ -1438,7 +1438,7 @@ __device__ __forceinline__ void wbvh_trip_impl(WbvhTrav& ts, const DSceneView<R>
         const bool ok = t >= 0.0f;
         ts.t_best = ok ? t : ts.t_best;
         ts.best = ok ? (int32_t)first : ts.best;
-        ts.leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+        ts.leaf = more ? ts.leaf - 7 : WBVH_NO_LEAF;  // ~((first + 1) << 3 | (more - 1)) = ~v - 7
     }
     // NRT_WBVH_UNIFIED: a lane holding both a leaf cursor and a node does both in one trip (a trip
     // runs both branches whenever the wave's lanes are mixed anyway); otherwise one or the other
@@ -1931,7 +1931,7 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
                 if (leaf_now) {
                     const uint32_t v = ~(uint32_t)leaf, first = v >> 3, more = v & 7u;
                     if (c.offer(load16(sc.wxprims + first), fr, first)) ts.t_best = c.bound * (1.0f + 0x1p-20f);
-                    leaf = more ? ~(int32_t)(((first + 1u) << 3) | (more - 1u)) : WBVH_NO_LEAF;
+                    leaf = more ? leaf - 7 : WBVH_NO_LEAF;  // ~((first + 1) << 3 | (more - 1)) = ~v - 7
                 }
                 if ((NRT_EXACT_IFIF == 2 || !leaf_now) && ts.node >= 0) {
                     wbvh4c_visit<R>(ts, sc, stk);
