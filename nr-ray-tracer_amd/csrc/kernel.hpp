@@ -3220,7 +3220,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const unsigned long long t1 = stamp();
             Rec<R> h;
             MatV<R> m;
-            V<R> contrib = mk(R(0), R(0), R(0));
+            V<R> contrib;  // (set by surface() wherever it is read: ends implies sh)
             bool scatter = false;
             if (sh) scatter = surface(traced, hit, hm, h, m, contrib);
             const unsigned long long t2 = stamp();
