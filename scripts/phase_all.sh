@@ -1,6 +1,9 @@
+# Phase profiles (PROF build of the f32 Philox loop, s_memtime stamps) of C4, C3 and C5 at spp 16:
+# the source of profiles/r04_phase_profile.json.  usage: bash scripts/phase_all.sh [out.json]
 set -o pipefail
 mkdir -p gpurun_out
-python - <<'PY' > gpurun_out/r4c_phase.json
+out=${1:-gpurun_out/phase_all.json}
+timeout -k 10 300 python - <<'PY' > $out
 import json, os, sys
 sys.path.insert(0, "nr-ray-tracer_amd")
 import nrt
@@ -11,4 +14,3 @@ for scene, w, h in (("scenes/utah-teapot-scene.json", 1024, 1024), ("scenes/eart
     out[scene] = s.phase_profile(precision="f32", rng="philox", trace="auto")
 print(json.dumps(out, indent=1))
 PY
-timeout -k 10 600 python scripts/ab_configs.py --reps 2 --out gpurun_out/r4c_ab.jsonl --lib A=nr-ray-tracer_amd/ab/on1/libnrt.so --lib B=nr-ray-tracer_amd/nrt/libnrt.so --cfg c3="--scene scenes/earth.toml --width 1920 --height 1080 --spp 128" --cfg c1big="--scene scenes/spheres.toml --width 1920 --height 1080 --spp 64" 2>&1 | tail -6
