@@ -7,8 +7,8 @@ tag=${1:-r04}
 part=${2:-f32a}
 case "$part" in
 f32a)
-bash scripts/profile.sh ${tag}_c5_f32_philox --steps 3 --warmup 1 && \
-bash scripts/profile.sh ${tag}_c4_f32_philox --scene scenes/utah-teapot-scene.json --steps 3 --warmup 1 && \
+bash scripts/profile.sh ${tag}_c5_f32_philox --steps 20 --warmup 2 && \
+bash scripts/profile.sh ${tag}_c4_f32_philox --scene scenes/utah-teapot-scene.json --steps 8 --warmup 2 && \
 bash scripts/profile.sh ${tag}_c3_f32_philox --scene scenes/earth.toml --width 1920 --height 1080 --spp 128 --steps 3 --warmup 1 ;;
 f32b)
 bash scripts/profile.sh ${tag}_c2_f32_philox --width 512 --height 512 --spp 64 --steps 5 --warmup 1 && \
