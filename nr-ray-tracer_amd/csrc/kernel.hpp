@@ -62,7 +62,7 @@ constexpr uint32_t CHACHA_LDS_BYTES = RING * BLOCK * 8u + 3u * BLOCK * 8u;
 // Persistent lanes with pixel claims of 2..8 (spp <= 64, render.hip): each wave stages the finished
 // pixels of up to STG_SLOTS claims in LDS (3 floats per pixel, then per claim its pixels left, first
 // pixel and size) and writes a claim out as one coalesced run once its last pixel is done, instead of
-// 12 scattered bytes per pixel (each costing a partial-line write-back: earth f64 87 -> 66 MB).
+// 12 scattered bytes per pixel (each costing a partial-line write-back: earth f64 66 -> 59 MB).
 constexpr uint32_t STG_SLOTS = 8, STG_PX = 8, NO_STG = 0xFFFFFFFFu;
 constexpr uint32_t STG_WAVE_WORDS = STG_SLOTS * (STG_PX * 3u + 3u);
 constexpr uint32_t STG_LDS_BYTES = (BLOCK / 64u) * STG_WAVE_WORDS * 4u;
@@ -2617,7 +2617,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             }
         }
     };
-    // dynamic LDS: [ChaCha8 ring | Philox pixel sums][world-BVH stack][staged scene]
+    // dynamic LDS: [ChaCha8 ring + pixel sums (+ claim staging) | Philox pool][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
     const uint32_t acc_bytes = G::exact_stream ? chacha_lds_bytes(p.exact_claim) - ring_bytes
                                                : philox_pool_bytes<MAXD>(p.wave_pixels);
