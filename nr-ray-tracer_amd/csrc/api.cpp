@@ -260,6 +260,12 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     p.exact_slots = spheres && f.wexact.size() <= 32 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_SLOTS")) p.exact_slots = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
+    // persistent lanes: fewest pixels per counter claim (0: render.hip's pick by spp); knob NRT_EXACT_CLAIM=1..64
+    p.exact_claim = 0;
+    if (const char* e = std::getenv("NRT_EXACT_CLAIM")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 64) p.exact_claim = (uint32_t)v;
+    }
     p.width = (uint32_t)c.width;
     p.height = (uint32_t)c.height;
     p.spp = c.samples_per_pixel < 1 ? 1u : (uint32_t)c.samples_per_pixel;

@@ -332,7 +332,10 @@ def test_chacha8_persistent_lanes_grid_invariant(scene, w, h, spp, precision, mo
     after pixel, each with its own stream and its samples in order (camera.rs:318-331), the pixels
     past the grid's first round handed out by per-XCD counters.  A pixel's value depends on its
     index alone, so the frame is the same bit for bit whatever the grid: one or three workgroups
-    (NRT_CHACHA_GRID) send nearly every pixel through the counters and their steal path."""
+    (NRT_CHACHA_GRID) send nearly every pixel through the counters and their steal path.  Nor does it
+    depend on how many pixels a wave claims per counter atomic (NRT_EXACT_CLAIM) or on the claims'
+    finished pixels being staged in LDS and written out per claim (claims of 2..8) or stored one by
+    one (1, or more than 8)."""
     s = load(scene, w, h, spp)
     base = s.render(precision=precision, rng="chacha8")
     assert np.isfinite(base).all() and base.max() > 0
@@ -340,6 +343,11 @@ def test_chacha8_persistent_lanes_grid_invariant(scene, w, h, spp, precision, mo
         monkeypatch.setenv("NRT_CHACHA_GRID", grid)
         img = s.render(precision=precision, rng="chacha8")
         assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), grid
+    monkeypatch.setenv("NRT_CHACHA_GRID", "1")
+    for claim in ("1", "5", "8", "64"):
+        monkeypatch.setenv("NRT_EXACT_CLAIM", claim)
+        img = s.render(precision=precision, rng="chacha8")
+        assert np.array_equal(img.view(np.uint32), base.view(np.uint32)), f"claim {claim}"
 
 
 def test_jit_require_refuses_the_generic_fallback(monkeypatch):
