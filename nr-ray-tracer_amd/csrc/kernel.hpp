@@ -40,6 +40,10 @@ constexpr int BLOCK = 256;
 #ifndef NRT_WBVH_UNIFIED
 #define NRT_WBVH_UNIFIED 1  // if-if trips: a visit and a primitive test in the same trip (C4 40.2 -> 34.6 ms)
 #endif
+#ifndef NRT_EXACT_SETPRIO
+#define NRT_EXACT_SETPRIO 3  // persistent-lane loop: wave priority of the shading step, 0 at the loop head
+                             // (0: never changed): earth f64 5.94 -> 5.79 ms, C5 f64 -0.3 %, C4 f64 +-0.5 %
+#endif
 #ifndef NRT_SETPRIO
 #define NRT_SETPRIO 3  // Philox loop: wave priority of the shading step, back to 0 at the loop head (0: never
                        // changed); a wave that has traced finishes its step first (C5 10.36 -> 10.28 ms,
@@ -2985,6 +2989,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         } else {
             bool fresh = true;
             while (true) {
+                if constexpr (NRT_EXACT_SETPRIO > 0) __builtin_amdgcn_s_setprio(0);
                 if (have && fresh && s >= p.spp) {  // the pixel's last sample has ended
                     finish_pixel();
                     have = false;
@@ -3010,6 +3015,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         p.exact_thread != 0);
                     t2 = stamp();
                 }
+                if constexpr (NRT_EXACT_SETPRIO > 0) __builtin_amdgcn_s_setprio(NRT_EXACT_SETPRIO);
                 fresh = !shade(traced, hit, hm);
                 if constexpr (PROF) {
                     const unsigned long long t3 = stamp();
