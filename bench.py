@@ -6,14 +6,23 @@ One "step" = one full frame, ending with the framebuffer in host memory (the
 reference times `scene.render`, which returns a host `Rgb32FImage`,
 app/commands/render.rs:57-62, camera.rs:342):
 
-  * every rank renders the image rows y = rank (mod N) with the HIP megakernel
+  * every GPU renders the image rows y = r (mod N) with the HIP megakernel
     (libnrt.so; the scene is resident in HBM since upload),
-  * N > 1: one RCCL gather (torch.distributed "nccl" = RCCL over xGMI) of the row
-    buffers to rank 0, which un-permutes them into the frame in HBM,
-  * rank 0 copies the frame to pinned host memory on a copy stream.  Frames are
-    double-buffered, so frame k's device-to-host copy overlaps frame k+1's render
+  * N > 1: one RCCL gather (over xGMI) of the row buffers to the first GPU, which
+    un-permutes them into the frame in HBM,
+  * the first GPU's frame is copied to pinned host memory on a copy stream.  Frames
+    are double-buffered, so frame k's device-to-host copy overlaps frame k+1's render
     (as a render loop would run); the timed region ends when the last frame is
     on the host.
+
+Two ways to run N > 1, both the same frame bit for bit (frame_sha256 on the line):
+  * one process (`python bench.py --gpus N`, no launcher): the library's own multi-GPU
+    render, nrt_render_opts.gpus = N (csrc/multi.hip: ncclCommInitAll over the N devices,
+    one ncclGather per frame) -- what a host calling the C ABI gets;
+  * one process per GPU (`python -m torch.distributed.run --nproc-per-node N ... bench.py
+    --gpus N`): rank r renders its rows, torch.distributed's "nccl" (= RCCL) gathers them
+    to rank 0 (nrt/shard.py).  `--backend gloo` without a launcher starts that launcher as
+    a child process (never exec) and forwards its line and exit status.
 
 The frame is fixed as N grows, so scaling is "strong".
 
@@ -25,7 +34,7 @@ bound that limits it, the FP32 (or FP64) VALU peak: achieved = SURVEY §8(d)'s
 algorithmic FLOPs per sample (oracle event counts x per-event costs,
 tests/golden/work_counts.json) x samples per launch / the kernel's HIP-event
 time on its launch stream.  The HBM figures the north star asks for sit beside
-it (`roofline.hbm`): framebuffer + scene bytes per launch over the same time,
+it (`roofline.hbm`): framebuffer + texel fetch bytes per launch over the same time,
 and rocprofv3 FETCH_SIZE/WRITE_SIZE traffic from profiles/pmc_summary.json,
 looked up by (scene, size, spp, precision, rng, trace).  The cpu_baseline leg
 times the oracle (the C++ f64 restatement; the Rust reference cannot be built
@@ -212,7 +221,7 @@ def work_block(wc, msamples_per_s, precision):
 
 # ------------------------------------------------------------------ main
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -228,15 +237,243 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=16)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="N > 1: nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = host-side gather, "
-                         "ranks may share a GPU (rehearses the N > 1 step on a one-GPU box)")
+                    help="one process per GPU: nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = "
+                         "host-side gather, ranks may share a GPU (rehearses the N > 1 step on a one-GPU box)")
+    ap.add_argument("--multi", default="auto", choices=["auto", "library", "ranks"],
+                    help="library = one process, the library's multi-GPU render (nrt_render_opts.gpus, RCCL inside "
+                         "libnrt.so; at N = 1 too, through the same RCCL code); ranks = one process per GPU under "
+                         "torch.distributed.run (started as a child process when this one has no launcher); auto = "
+                         "ranks under a launcher or with --backend gloo, library for N > 1 without a launcher, else "
+                         "the single-device path")
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
                          "prints one JSON line, no GPU is touched")
     ap.add_argument("--kernel-only", action="store_true",
                     help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
                          "sampled over a render dispatch see the render kernel alone")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_ranks_child(args):
+    """`--gpus N` one process per GPU without a launcher: torch.distributed.run as a CHILD process (this
+    process has not touched the GPU), its output passed through, its exit status returned."""
+    import socket
+
+    with socket.socket() as sk:  # a free rendezvous port on the loopback
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def load_scene(args, nrt):
+    old = os.getcwd()
+    os.chdir(os.path.join(ROOT, "tests", "golden"))  # scene files use CWD-relative paths
+    try:
+        t0 = time.perf_counter()
+        scene = nrt.Scene.load(args.scene, nrt.CameraConfig(width=args.width, height=args.height,
+                                                              samples_per_pixel=args.spp))
+        return scene, time.perf_counter() - t0
+    finally:
+        os.chdir(old)
+
+
+def kernel_variant_of(jit_before, jit_after, steps, mixed=False):
+    specialised = jit_after["launches"] - jit_before["launches"] >= steps
+    variant = "scene-specialised (hiprtc)" if specialised else "generic"
+    if mixed:
+        variant = "MIXED over ranks (scene-specialised on some, generic on others)"
+        print("bench.py: WARNING: ranks ran different kernel variants", file=sys.stderr, flush=True)
+    if jit_after["failed"]:
+        variant = "generic (scene-specialised build FAILED)"
+        print(f"bench.py: WARNING: {jit_after['failed']} scene-specialised kernel build(s) failed; the generic "
+              f"kernel was timed", file=sys.stderr, flush=True)
+    return variant
+
+
+def report(args, nrt, scene, *, n_gpus, rows, elapsed, kern_ms, d2h_ms, timings_s, frame_sha, jit_before, jit_after,
+           kernel_variant, parallelism, extra=None):
+    """The JSON line.  `rows` / `kern_ms`: the rows and HIP-event time of the launch the roofline prices
+    (the first GPU's)."""
+    cam = scene.camera
+    W, H, spp = cam.width, cam.height, cam.samples_per_pixel
+    samples = float(W) * H * spp
+    value = samples * args.steps / elapsed / 1e6
+    st = scene.stats()
+    key = {"scene": args.scene, "width": W, "height": H, "spp": spp, "precision": args.precision,
+           "rng": args.rng, "trace": args.trace, "n_gpus": n_gpus}
+    pmc = load_pmc(key)
+    traffic = pmc.get("hbm_bytes_per_launch")
+    wc = load_work(args.scene, W, H, spp)
+    # SURVEY §8(d) bytes per sample: 12/spp of framebuffer + texel_fetches/sample x the texel's bytes as
+    # stored (PAL16: the 2-byte index); the scene's records are a cache-resident working set, listed
+    # beside it (scene_bytes)
+    fb_bytes = rows * W * 12
+    texel_b = texel_payload_bytes(st)
+    fetches = 0.0 if wc is None else wc["per_sample"].get("texel_fetches", 0.0)
+    tex_bytes = fetches * texel_b * rows * W * spp
+    alg_bytes = fb_bytes + tex_bytes
+    hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+    prof_s = pmc.get("avg_ns", 0) / 1e9 if pmc else 0
+    counter_gbs = traffic / prof_s / 1e9 if traffic and prof_s else None
+    peak = VALU_PEAK_TFLOPS[args.precision]
+    if wc is not None:
+        flops_launch = wc["flops_per_sample"] * rows * W * spp  # this GPU's launch
+        achieved = flops_launch / (kern_ms / 1e3) / 1e12
+    else:
+        flops_launch, achieved = None, None
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n_gpus,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
+        "data": "reference scene file scenes/cornell-box-scene.json (no dataset; scene is the input)",
+        "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} spp={spp}", "scene": args.scene,
+                   "width": W, "height": H, "spp": spp, "ray_max_bounces": cam.ray_max_bounces,
+                   "rng": args.rng, "precision": args.precision, "trace": args.trace,
+                   "world_prims": st["world_prims"], "parallelism": parallelism,
+                   "timed_step": "render + (N>1) gather/un-permute" + (
+                       " (--kernel-only diagnostics: no device-to-host copy)" if args.kernel_only else
+                       " + device-to-host copy of the frame (pinned, double-buffered: frame k's copy overlaps "
+                       "frame k+1's render)")},
+        "roofline": {
+            "bound": "valu", "achieved": None if achieved is None else round(achieved, 3), "peak": peak,
+            "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / peak, 4),
+            "traffic": traffic,
+            "flops_per_launch": flops_launch, "kernel_ms": round(kern_ms, 3),
+            "flops_source": None if wc is None else
+            f"tests/golden/work_counts.json[{wc['name']}]: {wc['flops_per_sample']} algorithmic FLOPs/sample "
+            f"(oracle event counts x SURVEY §8(d) per-event costs) x {rows * W * spp} samples per launch",
+            "hbm": {"achieved": round(hbm_achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": round(alg_bytes),
+                    "algorithmic_bytes": {"framebuffer": fb_bytes, "texels": round(tex_bytes),
+                                          "texel_fetches_per_sample": fetches, "bytes_per_texel": texel_b,
+                                          "source": "SURVEY §8(d): 12/spp + texel_fetches x bytes per "
+                                                    "texel as stored, per sample"},
+                    "scene_bytes": scene_bytes(st, args.precision),
+                    "traffic": traffic,
+                    # rocprofv3 FETCH_SIZE + WRITE_SIZE per launch over the profiled kernel time
+                    # (profiles/pmc_summary.json, the committed profile of this variant and config)
+                    "counter_gbs": None if counter_gbs is None else round(counter_gbs, 3),
+                    "counter_frac": None if counter_gbs is None else counter_gbs / HBM_PEAK_GBS,
+                    "traffic_over_algorithmic": None if not traffic else round(traffic / alg_bytes, 3)},
+            "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
+                                            "valu_busy_est", "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
+                                            "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
+            "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
+                    "divergence; its compulsory HBM traffic is the framebuffer (plus texel fetches in textured "
+                    "scenes)"},
+        "work": work_block(wc, value, args.precision),
+        "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
+                       "frame_wall": round(elapsed / args.steps * 1e3, 3)},
+        # the reference times scene.render (render.rs:57-62): a one-shot render also pays the runtime start,
+        # the load, the upload and the scene-specialised kernel's build or disk-cache load, done here before
+        # the timed frames and reported on their own; first_frame = scene load start -> first frame on the host
+        "timings_s": timings_s,
+        "frame_sha256": frame_sha,
+        "build_id": nrt.build_id(),  # sha256 prefix of the sources libnrt.so was built from
+        # scene-specialised kernels (jit.hip): built with hiprtc or read from the disk cache in this process,
+        # renders using one; the timed frames ran on one only if every timed launch counted (a failed build
+        # falls back to the generic kernel, which is slower: then the line says so)
+        "jit": dict(jit_after, timed_launches=jit_after["launches"] - jit_before["launches"]),
+        "kernel_variant": kernel_variant,
+    }
+    if extra:
+        out.update(extra)
+    if not args.no_cpu_baseline and n_gpus == 1:
+        out["cpu_baseline"] = cpu_baseline(args)
+    elif not args.no_cpu_baseline:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
+def run_library(args):
+    """One process, N GPUs: the library's multi-GPU render (nrt_render_opts.gpus = N, csrc/multi.hip) into a
+    device frame on GPU 0, then the pinned, double-buffered host copy as in the single-device path."""
+    import torch
+    import nrt
+
+    N = args.gpus
+    ndev = torch.cuda.device_count()
+    if N > ndev:
+        raise SystemExit(f"--gpus {N} --multi library: {ndev} GPU(s) visible")
+    t0 = time.perf_counter()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    torch.zeros(1, device=dev)  # HIP runtime start (reported apart from the scene upload)
+    nrt.lib()
+    t_init = time.perf_counter() - t0
+    scene, t_load = load_scene(args, nrt)
+    t_first0 = time.perf_counter() - t_load
+    cam = scene.camera
+    W, H = cam.width, cam.height
+    t0 = time.perf_counter()
+    for d in range(N):
+        scene.upload(d)
+    t_upload = time.perf_counter() - t0
+    stream = torch.cuda.current_stream()
+    frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+    host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(2)]
+    copy_stream = torch.cuda.Stream(device=dev)
+    copied = [None, None]
+    cev = []
+
+    def step(k, timed):
+        slot = k % 2
+        if copied[slot] is not None:
+            stream.wait_event(copied[slot])  # frame `slot` was copied out two frames ago
+        scene.render_device(frames[slot].data_ptr(), H * W * 3, precision=args.precision, rng=args.rng, device=0,
+                            stream=stream.cuda_stream, trace=args.trace, gpus=N)
+        if not args.kernel_only:
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            copy_stream.wait_event(ready)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(copy_stream):
+                c0.record(copy_stream)
+                host[slot].view(-1).copy_(frames[slot].view(-1), non_blocking=True)
+                c1.record(copy_stream)
+            copied[slot] = c1
+            if timed:
+                cev.append((c0, c1))
+
+    first_frame = None
+    for k in range(args.warmup):
+        step(k, False)
+        if k == 0:
+            torch.cuda.synchronize()
+            first_frame = time.perf_counter() - t_first0
+    torch.cuda.synchronize()
+    jit_before = nrt.jit_stats()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, True)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tm = scene.render_timings()  # the last timed frame's per-device kernel and gather times
+    d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
+    jit_after = nrt.jit_stats()
+    last = host[(args.warmup + args.steps - 1) % 2].numpy()
+    frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
+    rows = scene.rows_selected(H, 0, N)
+    report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=tm["kernel_ms"][0], d2h_ms=d2h_ms,
+           timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
+                      "upload": round(t_upload, 4), "jit_compile": jit_after["compile_s"],
+                      "first_frame": None if first_frame is None else round(first_frame, 4)},
+           frame_sha=frame_sha, jit_before=jit_before, jit_after=jit_after,
+           kernel_variant=kernel_variant_of(jit_before, jit_after, args.steps * N),
+           parallelism=f"rows interleaved over {N} GPU(s) of one process, one RCCL ncclGather to GPU 0 "
+                       f"(libnrt.so nrt_render_opts.gpus)",
+           extra={"multi_gpu": {"path": "library", "kernel_ms_per_gpu": [round(x, 3) for x in tm["kernel_ms"]],
+                                "gather_unpermute_ms": round(tm["gather_ms"], 3),
+                                "note": "HIP-event times of the last timed frame (nrt_render_timings)"}})
+
+
+def main():
+    args = parse_args()
     if args.cpu_only:
         cpu = cpu_baseline(args)
         print(json.dumps({"metric": "Msamples/sec (CPU baseline, oracle)", "value": cpu["value"], "unit": "Msamples/s",
@@ -245,8 +482,26 @@ def main():
                                                                "scene": args.scene, "width": args.width,
                                                                "height": args.height, "spp": args.spp},
                           "cpu_baseline": cpu}), flush=True)
-        return
+        return 0
 
+    launched = "WORLD_SIZE" in os.environ
+    multi = args.multi
+    if multi == "auto":
+        multi = "ranks" if launched or (args.gpus > 1 and args.backend == "gloo") else (
+            "library" if args.gpus > 1 else "ranks")
+    if multi == "library":
+        if launched:
+            raise SystemExit("--multi library runs in one process: start it without torch.distributed.run")
+        return run_library(args)
+    if not launched and args.gpus > 1:
+        # one process per GPU, no launcher: torch.distributed.run as a child (nothing has touched the GPU)
+        return launch_ranks_child(args)
+    return run_ranks(args)
+
+
+def run_ranks(args):
+    """One process per GPU (N = 1: this process alone): rank r renders rows y = r (mod N); N > 1: one
+    torch.distributed gather (RCCL with --backend nccl) to rank 0 and a device un-permute there."""
     import torch
     import torch.distributed as dist
     import nrt
@@ -255,31 +510,28 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1:
-        raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} under a launcher of {world} process(es)")
+    t0 = time.perf_counter()
     ndev = torch.cuda.device_count()
     if args.backend == "nccl" and local >= ndev:
         raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but {ndev} GPU(s) visible (nccl needs one GPU per rank)")
     local = local % ndev  # gloo: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    torch.zeros(1, device=dev)  # HIP runtime start (reported apart from the scene upload)
+    nrt.lib()
+    t_init = time.perf_counter() - t0
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
-    old = os.getcwd()
-    os.chdir(os.path.join(ROOT, "tests", "golden"))  # scene files use CWD-relative paths
-    try:
-        t0 = time.perf_counter()
-        scene = nrt.Scene.load(args.scene, nrt.CameraConfig(width=args.width, height=args.height,
-                                                              samples_per_pixel=args.spp))
-        t_load = time.perf_counter() - t0
-    finally:
-        os.chdir(old)
+    scene, t_load = load_scene(args, nrt)
+    t_first0 = time.perf_counter() - t_load
     cam = scene.camera
-    W, H, spp = cam.width, cam.height, cam.samples_per_pixel
+    W, H = cam.width, cam.height
     t0 = time.perf_counter()
     scene.upload(local)
     t_upload = time.perf_counter() - t0
@@ -332,8 +584,12 @@ def main():
             if timed:
                 cev.append((c0, c1))
 
+    first_frame = None
     for k in range(args.warmup):
         step(k, False)
+        if k == 0:
+            torch.cuda.synchronize()
+            first_frame = time.perf_counter() - t_first0
     torch.cuda.synchronize()
     jit_before = nrt.jit_stats()  # the first render of the scene in a world mode built its kernel (warm-up)
     if world > 1:
@@ -358,108 +614,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
         mixed = float(t[2]) != -float(t[3])
-
-    kernel_variant = "scene-specialised (hiprtc)" if specialised else "generic"
-    if mixed:
-        kernel_variant = "MIXED over ranks (scene-specialised on some, generic on others)"
-        print("bench.py: WARNING: ranks ran different kernel variants", file=sys.stderr, flush=True)
-    if jit_after["failed"]:
-        kernel_variant = "generic (scene-specialised build FAILED)"
-        print(f"bench.py: WARNING: {jit_after['failed']} scene-specialised kernel build(s) failed; the generic "
-              f"kernel was timed", file=sys.stderr, flush=True)
+    variant = kernel_variant_of(jit_before, jit_after, args.steps, mixed)
     if lead:
         last = host[(args.warmup + args.steps - 1) % 2].numpy()
         frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
-        samples = float(W) * H * spp
-        value = samples * args.steps / elapsed / 1e6
-        st = scene.stats()
-        key = {"scene": args.scene, "width": W, "height": H, "spp": spp, "precision": args.precision,
-               "rng": args.rng, "trace": args.trace, "n_gpus": world}
-        pmc = load_pmc(key)
-        traffic = pmc.get("hbm_bytes_per_launch")
-        wc = load_work(args.scene, W, H, spp)
-        # SURVEY §8(d) bytes per sample: 12/spp of framebuffer + texel_fetches/sample x the texel's bytes,
-        # priced at the bytes per texel actually stored (3 for file images); the scene's records are a
-        # cache-resident working set, listed beside it (scene_bytes)
-        fb_bytes = rows * W * 12
-        texel_b = texel_payload_bytes(st)
-        fetches = 0.0 if wc is None else wc["per_sample"].get("texel_fetches", 0.0)
-        tex_bytes = fetches * texel_b * rows * W * spp
-        alg_bytes = fb_bytes + tex_bytes
-        hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        prof_s = pmc.get("avg_ns", 0) / 1e9 if pmc else 0
-        counter_gbs = traffic / prof_s / 1e9 if traffic and prof_s else None
-        peak = VALU_PEAK_TFLOPS[args.precision]
-        if wc is not None:
-            flops_launch = wc["flops_per_sample"] * rows * W * spp  # this rank's launch
-            achieved = flops_launch / (kern_ms / 1e3) / 1e12
-        else:
-            flops_launch, achieved = None, None
-        out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
-            "data": "reference scene file scenes/cornell-box-scene.json (no dataset; scene is the input)",
-            "config": {"workload": f"{os.path.basename(args.scene)} {W}x{H} spp={spp}", "scene": args.scene,
-                       "width": W, "height": H, "spp": spp, "ray_max_bounces": cam.ray_max_bounces,
-                       "rng": args.rng, "precision": args.precision, "trace": args.trace,
-                       "world_prims": st["world_prims"],
-                       "parallelism": f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
-                       "timed_step": "render + (N>1) gather/un-permute" + (
-                           " (--kernel-only diagnostics: no device-to-host copy)" if args.kernel_only else
-                           " + device-to-host copy of the frame (pinned, double-buffered: frame k's copy overlaps "
-                           "frame k+1's render)")},
-            "roofline": {
-                "bound": "valu", "achieved": None if achieved is None else round(achieved, 3), "peak": peak,
-                "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / peak, 4),
-                "traffic": traffic,
-                "flops_per_launch": flops_launch, "kernel_ms": round(kern_ms, 3),
-                "flops_source": None if wc is None else
-                f"tests/golden/work_counts.json[{wc['name']}]: {wc['flops_per_sample']} algorithmic FLOPs/sample "
-                f"(oracle event counts x SURVEY §8(d) per-event costs) x {rows * W * spp} samples per launch",
-                "hbm": {"achieved": round(hbm_achieved, 6), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": round(alg_bytes),
-                        "algorithmic_bytes": {"framebuffer": fb_bytes, "texels": round(tex_bytes),
-                                              "texel_fetches_per_sample": fetches, "bytes_per_texel": texel_b,
-                                              "source": "SURVEY §8(d): 12/spp + texel_fetches x bytes per "
-                                                        "texel as stored, per sample"},
-                        "scene_bytes": scene_bytes(st, args.precision),
-                        "traffic": traffic,
-                        # rocprofv3 FETCH_SIZE + WRITE_SIZE per launch over the profiled kernel time
-                        # (profiles/pmc_summary.json, the committed profile of this variant and config)
-                        "counter_gbs": None if counter_gbs is None else round(counter_gbs, 3),
-                        "counter_frac": None if counter_gbs is None else counter_gbs / HBM_PEAK_GBS,
-                        "traffic_over_algorithmic": None if not traffic else round(traffic / alg_bytes, 3)},
-                "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
-                                                "valu_busy_est", "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
-                                                "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
-                "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "
-                        "divergence; its compulsory HBM traffic is the framebuffer (plus texel fetches in textured "
-                        "scenes)"},
-            "work": work_block(wc, value, args.precision),
-            "timings_ms": {"kernel_device_only": round(kern_ms, 3), "d2h_copy": round(d2h_ms, 3),
-                           "frame_wall": round(elapsed / args.steps * 1e3, 3)},
-            # the reference times scene.render (render.rs:57-62): a one-shot render of a scene would also pay
-            # the scene-specialised kernel's compile, done here in the warm-up and reported on its own
-            "timings_s": {"scene_load_and_bvh": round(t_load, 4), "upload": round(t_upload, 4),
-                          "jit_compile": jit_after["compile_s"]},
-            "frame_sha256": frame_sha,
-            "build_id": nrt.build_id(),  # sha256 prefix of the sources libnrt.so was built from
-            # scene-specialised kernels (jit.hip): built with hiprtc in this process, renders using one; the
-            # timed frames ran on one only if every timed launch counted (a failed build falls back to the
-            # generic kernel, which is slower: then the line says so)
-            "jit": dict(jit_after, timed_launches=jit_after["launches"] - jit_before["launches"]),
-            "kernel_variant": kernel_variant,
-        }
-        if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args)
-        elif not args.no_cpu_baseline:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
+        report(args, nrt, scene, n_gpus=world, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
+               timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
+                          "upload": round(t_upload, 4), "jit_compile": jit_after["compile_s"],
+                          "first_frame": None if first_frame is None else round(first_frame, 4)},
+               frame_sha=frame_sha, jit_before=jit_before, jit_after=jit_after, kernel_variant=variant,
+               parallelism=f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
+               extra={"multi_gpu": {"path": "ranks", "backend": args.backend}} if world > 1 else None)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

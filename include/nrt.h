@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 5
+#define NRT_ABI_VERSION 6
 
 enum {
     NRT_OK = 0,
@@ -114,11 +114,19 @@ typedef struct {
 typedef struct {
     uint32_t precision;  /* nrt_precision */
     uint32_t rng;        /* nrt_rng */
-    int32_t device;      /* HIP device ordinal; -1 = current device */
+    int32_t device;      /* HIP device ordinal; -1 = current device (gpus >= 1: -1 = device 0) */
     uint32_t row_offset; /* render image rows y = row_offset + k*row_stride ... */
     uint32_t row_stride; /* ... (0 or 1: every row); output rows are compact */
     uint32_t trace;      /* nrt_trace (f32 kernel only) */
-    uint32_t reserved[2];
+    /* 0: one device (`device`), the rows above.  N >= 1: the whole frame over the N devices
+     * device .. device+N-1 of this process (Camera::render's one call over the whole machine,
+     * lib/camera.rs:315-316): device first+r renders rows y = r (mod N) into its HBM,
+     * one RCCL ncclGather (librccl, dlopen'ed) brings the shards to the first device, which
+     * un-permutes them into the frame.  Needs row_offset 0 and row_stride <= 1; the frame is the
+     * same bits as gpus = 0 (pixels and their RNG streams do not depend on the device).  The
+     * scene owns the communicators and shard buffers (created on first use, freed with it). */
+    uint32_t gpus;
+    uint32_t reserved;
 } nrt_render_opts;
 
 typedef struct {
@@ -132,7 +140,11 @@ typedef struct {
                                 (else AUTO takes the world BVH, which compares tie keys) */
     uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
     uint32_t reserved;
-    uint64_t texel_bytes;    /* HBM bytes of the texel array (file images: 3 B per texel in 128-B tiles of 8 x 5) */
+    /* HBM bytes of the texel array: image textures as stored (PAL16, the default for file images
+     * whose bands fit: a 2-byte palette index per texel in 8 x 8 tiles plus an RGBA8 palette per
+     * band; else RGB8T, 3 B per texel in 128-B tiles of 8 x 5; RGBA8 tiles; RGB32F for constructor
+     * images with values other than k/255) plus the Perlin permutation tables of Noise / Marble */
+    uint64_t texel_bytes;
 } nrt_scene_stats;
 /* Exact-kernel traversal (same closest hit and tie-break as BVH::hit, object.rs:89-121):
  *   BVH      the reference tree, box by box
@@ -149,11 +161,16 @@ int nrt_abi_version(void);
 const char* nrt_build_id(void);
 /* Scene-specialised kernels (built with hiprtc, loaded lazily, when a scene is first rendered
  * in an f32 world mode; NRT_JIT=0 turns them off, NRT_JIT=require makes a failed build an
- * error of the render call instead of a fallback to the generic kernel).  The first such render of a scene in a
- * process pays the compile (~1 s) inside the render call.  out[0] = kernels built in this
- * process, out[1] = renders that used one, out[2] = builds that failed (the generic kernel
- * rendered instead: slower, and its f32 frames may differ in the last bits), out[3] = compile
- * wall time in ns; the first min(n, 4) are written.  No reference counterpart. */
+ * error of the render call instead of a fallback to the generic kernel).  The first such render
+ * of a scene pays the compile (0.2-0.5 s) inside the render call, unless the on-disk code-object
+ * cache holds it (NRT_JIT_CACHE = a directory, default $XDG_CACHE_HOME/nrt-jit or
+ * ~/.cache/nrt-jit; "0" turns it off): keyed by the library's build id, the architecture, the
+ * template arguments and the compile options, written atomically and verified on load.
+ * out[0] = kernels built by hiprtc in this process, out[1] = renders that used a specialised
+ * kernel, out[2] = builds that failed (the generic kernel rendered instead: slower, the same
+ * frame bit for bit), out[3] = compile + load wall time in ns, out[4] = code objects taken from
+ * the disk cache, out[5] = module loads that failed and were retried; the first min(n, 6) are
+ * written.  No reference counterpart. */
 int nrt_jit_stats(uint64_t* out, size_t n);
 /* Tests: compile render_kernel<targs> with hiprtc from the embedded headers, no GPU needed
  * (nothing is loaded); *code_bytes = the code object's size. */
@@ -236,6 +253,14 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
  * asynchronous: returns after enqueueing. */
 int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
                       float* dev_out_rgb, size_t out_len, void* hip_stream);
+/* With opts->gpus = N >= 1: dev_out_rgb (W*H*3 f32) and hip_stream belong to the first device;
+ * every device's render and the gather are enqueued and the call returns; hip_stream waits for
+ * the frame, which is written only after hip_stream's prior work.  Consecutive calls pipeline:
+ * frame k+1's renders may start while frame k's last paths, gather and un-permute run. */
+/* HIP-event times (ms) of the scene's last gpus >= 1 render (waits for it): out[d] = the render
+ * kernel on device first+d, d < N; out[N] = the gather + un-permute on the first device (from its
+ * own render's end, so the slowest device's lag is in it).  *count = N + 1; at most n written. */
+int nrt_render_timings(const nrt_scene* scene, float* out, size_t n, size_t* count);
 /* Number of rows selected by opts for an image of `height` rows. */
 uint32_t nrt_rows_selected(uint32_t height, const nrt_render_opts* opts);
 /* Upload the flattened scene to `device` now (otherwise done on first render). */

@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -23,7 +24,11 @@ struct nrt_scene {
     FlatScene flat;
     std::mutex mu;
     std::vector<DeviceScene*> per_device;  // index = HIP ordinal
+    // multi-GPU renders (nrt_render_opts.gpus): one context per (first device, N), the last used
+    std::map<std::pair<int, int>, MultiRender*> multi;
+    MultiRender* last_multi = nullptr;
     ~nrt_scene() {
+        for (auto& kv : multi) gpu_multi_free(kv.second);  // (before the device scenes they render)
         for (DeviceScene* d : per_device) gpu_free_scene(d);
     }
 };
@@ -333,6 +338,26 @@ void check_opts(const nrt_render_opts* o) {
     if (o->precision > NRT_PRECISION_F32) throw std::invalid_argument("unknown precision");
     if (o->rng > NRT_RNG_PHILOX) throw std::invalid_argument("unknown rng");
     if (o->trace > NRT_TRACE_WORLD_BVH) throw std::invalid_argument("unknown trace mode");
+    if (o->gpus && (o->row_offset != 0 || o->row_stride > 1))
+        throw std::invalid_argument("gpus >= 1 renders the whole frame: row_offset must be 0 and row_stride <= 1");
+}
+
+// The multi-GPU context of opts (gpus >= 1): devices first .. first + gpus - 1, each with the
+// scene uploaded, one RCCL communicator each (multi.hip).
+MultiRender* multi_render(nrt_scene* s, const nrt_render_opts* o) {
+    const int n = gpu_device_count();
+    if (n <= 0) throw std::runtime_error("HIP error in device query: no GPU device available");
+    const int first = o->device < 0 ? 0 : o->device;
+    if ((int64_t)first + (int64_t)o->gpus > (int64_t)n)
+        throw std::invalid_argument("gpus = " + std::to_string(o->gpus) + " from device " + std::to_string(first) +
+                                    ": only " + std::to_string(n) + " device(s) visible");
+    std::vector<DeviceScene*> scenes;
+    for (uint32_t d = 0; d < o->gpus; ++d) scenes.push_back(device_scene(s, first + (int)d));
+    std::lock_guard<std::mutex> lock(s->mu);
+    MultiRender*& m = s->multi[std::make_pair(first, (int)o->gpus)];
+    if (!m) m = gpu_multi_create(scenes);
+    s->last_multi = m;
+    return m;
 }
 
 }  // namespace
@@ -371,8 +396,8 @@ int nrt_jit_stats(uint64_t* out, size_t n) {
     return guarded(NRT_E_INVALID, [&]() {
         if (!out && n) throw std::invalid_argument("null output");
         const JitCounts c = gpu_jit_counts();
-        const uint64_t v[4] = {c.compiled, c.launches, c.failed, c.compile_ns};
-        for (size_t k = 0; k < n && k < 4; ++k) out[k] = v[k];
+        const uint64_t v[6] = {c.compiled, c.launches, c.failed, c.compile_ns, c.disk_hits, c.load_retries};
+        for (size_t k = 0; k < n && k < 6; ++k) out[k] = v[k];
         return NRT_OK;
     });
 }
@@ -572,6 +597,12 @@ int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nr
         const uint32_t rows = rows_selected((uint32_t)camera->height, opts);
         RenderParams p = make_params(*camera, opts, rows, scene->flat);
         if (out_len < (size_t)rows * p.width * 3) throw std::invalid_argument("output buffer too small");
+        if (opts && opts->gpus) {
+            if (rows == 0) return NRT_OK;
+            MultiRender* m = multi_render(const_cast<nrt_scene*>(scene), opts);
+            gpu_multi_render_device(m, p, opts->precision, opts->rng, opts->trace, dev_out_rgb, hip_stream);
+            return NRT_OK;
+        }
         const int dev = resolve_device(opts);
         DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
         p.out = dev_out_rgb;
@@ -590,6 +621,12 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
         const size_t n = (size_t)rows * p.width * 3;
         if (out_len < n) throw std::invalid_argument("output buffer too small");
         if (n == 0) return NRT_OK;
+        if (opts && opts->gpus) {  // the whole frame over opts->gpus devices, one RCCL gather
+            MultiRender* m = multi_render(const_cast<nrt_scene*>(scene), opts);
+            gpu_multi_render_host(m, p, opts->precision, opts->rng, opts->trace, out_rgb);
+            if (progress) progress(user, p.pixel_end);
+            return NRT_OK;
+        }
         const int dev = resolve_device(opts);
         DeviceScene* ds = device_scene(const_cast<nrt_scene*>(scene), dev);
         void* d = device_alloc(n * sizeof(float), dev);
@@ -615,6 +652,21 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
             throw;
         }
         device_free(d, dev);
+        return NRT_OK;
+    });
+}
+
+int nrt_render_timings(const nrt_scene* scene, float* out, size_t n, size_t* count) {
+    return guarded(NRT_E_INVALID, [&]() {
+        if (!scene || (!out && n)) throw std::invalid_argument("null argument");
+        MultiRender* m = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(const_cast<nrt_scene*>(scene)->mu);
+            m = scene->last_multi;
+        }
+        if (!m) throw std::invalid_argument("no multi-GPU render (gpus >= 1) of this scene yet");
+        const size_t c = gpu_multi_timings(m, out, n);
+        if (count) *count = c;
         return NRT_OK;
     });
 }

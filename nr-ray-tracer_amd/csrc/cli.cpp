@@ -21,7 +21,6 @@
 #include <cstring>
 #include <regex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "nrt.h"
@@ -320,32 +319,10 @@ int main(int argc, char** argv) {
     int ndev = nrt_device_count();
     if (gpus < 1) gpus = 1;
     if (gpus > ndev) die("requested " + std::to_string(gpus) + " GPUs, " + std::to_string(ndev) + " visible");
-    if (gpus == 1) {
-        if (nrt_render(sc, &cam, &opts, img.data(), img.size(), nullptr, nullptr) != NRT_OK) die(nrt_last_error());
-    } else {
-        // one host thread per device, rows interleaved r = g (mod N), then unpermuted
-        std::vector<std::vector<float>> parts((size_t)gpus);
-        std::vector<std::string> errs((size_t)gpus);
-        std::vector<std::thread> th;
-        for (int g = 0; g < gpus; ++g) {
-            th.emplace_back([&, g]() {
-                nrt_render_opts o = opts;
-                o.device = g;
-                o.row_offset = (uint32_t)g;
-                o.row_stride = (uint32_t)gpus;
-                const uint32_t rows = nrt_rows_selected(H, &o);
-                parts[(size_t)g].resize((size_t)rows * W * 3);
-                if (nrt_render(sc, &cam, &o, parts[(size_t)g].data(), parts[(size_t)g].size(), nullptr, nullptr) != NRT_OK)
-                    errs[(size_t)g] = nrt_last_error();
-            });
-        }
-        for (auto& t : th) t.join();
-        for (auto& e : errs) if (!e.empty()) die(e);
-        for (uint32_t y = 0; y < H; ++y) {
-            const auto& part = parts[y % (uint32_t)gpus];
-            memcpy(&img[(size_t)y * W * 3], &part[(size_t)(y / (uint32_t)gpus) * W * 3], (size_t)W * 3 * sizeof(float));
-        }
-    }
+    // --gpus N > 1: the library's multi-GPU render (nrt_render_opts.gpus): rows interleaved over
+    // devices 0 .. N-1, one RCCL gather to device 0, un-permuted there
+    if (gpus > 1) opts.gpus = (uint32_t)gpus;
+    if (nrt_render(sc, &cam, &opts, img.data(), img.size(), nullptr, nullptr) != NRT_OK) die(nrt_last_error());
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (verbose) {
         const double samples = (double)W * H * (double)cam.samples_per_pixel;

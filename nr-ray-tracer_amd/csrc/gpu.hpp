@@ -4,6 +4,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "render_params.hpp"
 
@@ -11,6 +12,24 @@ namespace nrt {
 
 struct FlatScene;
 struct DeviceScene;
+struct MultiRender;
+
+// Multi-GPU render in one process (multi.hip): scenes[d] on device first + d (consecutive), one
+// RCCL communicator per device (ncclCommInitAll), rows y = d (mod N) on device d, one ncclGather
+// to the first device and a row un-permute there.  p is the full-frame RenderParams.
+MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes);  // throws (no librccl, HIP/RCCL errors)
+void gpu_multi_free(MultiRender* m);
+int gpu_multi_first(const MultiRender* m);
+int gpu_multi_count(const MultiRender* m);
+// asynchronous: dev_out (first device) is written after `stream`'s prior work, and `stream` waits for it
+void gpu_multi_render_device(MultiRender* m, const RenderParams& p, uint32_t precision, uint32_t rng, uint32_t trace,
+                             float* dev_out, void* stream);
+// synchronous: the frame lands in host memory
+void gpu_multi_render_host(MultiRender* m, const RenderParams& p, uint32_t precision, uint32_t rng, uint32_t trace,
+                           float* host_out);
+// HIP-event times (ms) of the last frame: out[d] = device first + d's render kernel, out[N] = the
+// gather + un-permute on the first device; returns N + 1 (entries past n are not written)
+size_t gpu_multi_timings(MultiRender* m, float* out, size_t n);
 
 int gpu_device_count();
 DeviceScene* gpu_upload_scene(const FlatScene& fs, int device);  // throws std::runtime_error
@@ -24,7 +43,7 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
 int gpu_fast_maxd(const DeviceScene* ds, uint32_t trace);
 // First `count` draws of `lanes` consecutive streams starting at stream0 (tests).
 struct JitCounts {
-    uint64_t compiled, launches, failed, compile_ns;
+    uint64_t compiled, launches, failed, compile_ns, disk_hits, load_retries;
 };
 JitCounts gpu_jit_counts();  // scene-specialised kernels (jit.hip)
 uint64_t gpu_jit_compile_only(const char* targs, std::string* log);

@@ -1314,15 +1314,14 @@ __device__ __forceinline__ void wbvh4c_visit_nd(WbvhTrav& t, const DBvh4cNode& n
     // reads either half as an f16 operand: (1024 + q) * A + (B - 1024 A).  The folded offset
     // rounds B - 1024 A to f32, an error of ~2^-14 of a quantization step in t (the decode's own
     // f32 rounding is of that order).
-    uint32_t k64, sel01, sel23;
-    asm volatile("s_mov_b32 %0, 0x64646464" : "=s"(k64));
-    asm volatile("s_mov_b32 %0, 0x04010400" : "=s"(sel01));
-    asm volatile("s_mov_b32 %0, 0x04030402" : "=s"(sel23));
+    // (gfx9 VOP3: one SGPR or literal per instruction, so the 0x64 bytes sit in a VGPR and the
+    // selector in an SGPR)
+    const uint32_t k64 = 0x64646464u, sel01 = 0x04010400u, sel23 = 0x04030402u;
     const float Cx = __builtin_fmaf(-1024.0f, Ax, Bx), Cy = __builtin_fmaf(-1024.0f, Ay, By),
                 Cz = __builtin_fmaf(-1024.0f, Az, Bz);
     auto pairs = [&](uint32_t w, uint32_t sel) {
         uint32_t r;
-        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "s"(k64), "v"(w), "s"(sel));
+        asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(k64), "v"(w), "s"(sel));
         return r;
     };
     auto mix_lo = [](uint32_t h, float a, float c) {

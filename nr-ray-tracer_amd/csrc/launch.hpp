@@ -37,6 +37,8 @@ struct JitStats {
     uint64_t launches = 0;    // renders that used one
     uint64_t failed = 0;      // builds that failed (the generic kernel ran instead)
     uint64_t compile_ns = 0;  // wall time spent in hiprtc + module load
+    uint64_t disk_hits = 0;   // code objects read from the on-disk cache instead of compiled
+    uint64_t load_retries = 0;  // module loads that failed and were left to a later render
 };
 void* jit_render_kernel(const std::string& targs, int device);
 // throws under NRT_JIT=require (jit.hip): called when jit_render_kernel returned null

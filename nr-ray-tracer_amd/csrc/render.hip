@@ -325,7 +325,7 @@ uint64_t gpu_jit_compile_only(const char* targs, std::string* log) { return jit_
 
 JitCounts gpu_jit_counts() {
     const JitStats s = jit_stats();
-    return JitCounts{s.compiled, s.launches, s.failed, s.compile_ns};
+    return JitCounts{s.compiled, s.launches, s.failed, s.compile_ns, s.disk_hits, s.load_retries};
 }
 
 void gpu_rng_probe(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* host_out) {

@@ -62,7 +62,7 @@ class _Camera(C.Structure):
 
 class _RenderOpts(C.Structure):
     _fields_ = [("precision", C.c_uint32), ("rng", C.c_uint32), ("device", C.c_int32), ("row_offset", C.c_uint32),
-                ("row_stride", C.c_uint32), ("trace", C.c_uint32), ("reserved", C.c_uint32 * 2)]
+                ("row_stride", C.c_uint32), ("trace", C.c_uint32), ("gpus", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class _SceneStats(C.Structure):
@@ -120,6 +120,7 @@ SIGNATURES = {
                              C.c_size_t, PROGRESS_FN, C.c_void_p]),
     "nrt_render_device": (C.c_int, [C.c_void_p, C.POINTER(_Camera), C.POINTER(_RenderOpts), C.c_void_p, C.c_size_t,
                                     C.c_void_p]),
+    "nrt_render_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_size_t)]),
     "nrt_rows_selected": (C.c_uint32, [C.c_uint32, C.POINTER(_RenderOpts)]),
     "nrt_scene_upload": (C.c_int, [C.c_void_p, C.c_int32]),
     "nrt_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(_SceneStats)]),
@@ -191,12 +192,13 @@ def build_id() -> str:
 
 
 def jit_stats() -> dict:
-    """Scene-specialised kernels (nrt_jit_stats): built in this process, renders using one, builds that
-    failed (the generic kernel rendered instead), seconds spent compiling."""
-    out = (C.c_uint64 * 4)()
-    _check(lib().nrt_jit_stats(out, 4))
+    """Scene-specialised kernels (nrt_jit_stats): built by hiprtc in this process, renders using one,
+    builds that failed (the generic kernel rendered instead), seconds spent compiling or loading, code
+    objects read from the on-disk cache, module loads left to a later render."""
+    out = (C.c_uint64 * 6)()
+    _check(lib().nrt_jit_stats(out, 6))
     return {"compiled": int(out[0]), "launches": int(out[1]), "failed": int(out[2]),
-            "compile_s": round(int(out[3]) * 1e-9, 4)}
+            "compile_s": round(int(out[3]) * 1e-9, 4), "disk_hits": int(out[4]), "load_retries": int(out[5])}
 
 
 def debug_jit_compile(targs: str) -> int:
@@ -337,7 +339,7 @@ class CameraBuilder:
 
 
 def _opts(precision: str, rng: str, device: int, row_offset: int, row_stride: int,
-          trace: str = "auto") -> _RenderOpts:
+          trace: str = "auto", gpus: int = 0) -> _RenderOpts:
     if precision not in PRECISION:
         raise ValueError(f"precision must be one of {list(PRECISION)}")
     if rng not in RNG:
@@ -347,6 +349,7 @@ def _opts(precision: str, rng: str, device: int, row_offset: int, row_stride: in
     o = _RenderOpts()
     o.precision, o.rng, o.device = PRECISION[precision], RNG[rng], device
     o.row_offset, o.row_stride, o.trace = row_offset, row_stride, TRACE[trace]
+    o.gpus = gpus
     return o
 
 
@@ -401,12 +404,13 @@ class Scene:
 
     def render(self, camera: Optional[Camera] = None, precision: str = "f64", rng: str = "chacha8",
                device: int = -1, row_offset: int = 0, row_stride: int = 1,
-               progress: Optional[Callable[[int], None]] = None, trace: str = "auto") -> np.ndarray:
-        """Camera::render -> Rgb32FImage as float32 array (rows, W, 3)."""
+               progress: Optional[Callable[[int], None]] = None, trace: str = "auto", gpus: int = 0) -> np.ndarray:
+        """Camera::render -> Rgb32FImage as float32 array (rows, W, 3).  gpus = N >= 1: the whole frame
+        over devices device .. device+N-1 (device -1: 0), one RCCL gather (nrt_render_opts.gpus)."""
         cam = camera or self.camera
         if cam is None:
             raise ValueError("no camera")
-        o = _opts(precision, rng, device, row_offset, row_stride, trace)
+        o = _opts(precision, rng, device, row_offset, row_stride, trace, gpus)
         rows = lib().nrt_rows_selected(cam.height, C.byref(o))
         out = np.empty((rows, cam.width, 3), dtype=np.float32)
         cb = PROGRESS_FN(lambda _u, n: progress(n)) if progress else PROGRESS_FN()
@@ -445,12 +449,24 @@ class Scene:
 
     def render_device(self, out_ptr: int, out_len: int, camera: Optional[Camera] = None, precision: str = "f32",
                       rng: str = "philox", device: int = -1, row_offset: int = 0, row_stride: int = 1,
-                      stream: int = 0, trace: str = "auto") -> None:
-        """Enqueue a render into device memory (e.g. a torch tensor's data_ptr) on a HIP stream."""
+                      stream: int = 0, trace: str = "auto", gpus: int = 0) -> None:
+        """Enqueue a render into device memory (e.g. a torch tensor's data_ptr) on a HIP stream; gpus = N
+        >= 1: the whole frame over N devices into out_ptr on the first (nrt_render_opts.gpus)."""
         cam = camera or self.camera
-        o = _opts(precision, rng, device, row_offset, row_stride, trace)
+        o = _opts(precision, rng, device, row_offset, row_stride, trace, gpus)
         _check(lib().nrt_render_device(self._h, C.byref(cam._c()), C.byref(o), C.c_void_p(out_ptr), out_len,
                                        C.c_void_p(stream)))
+
+
+    def render_timings(self) -> dict:
+        """HIP-event times of the last gpus >= 1 render (nrt_render_timings): per-device render kernel ms
+        and the gather + un-permute ms on the first device."""
+        n = C.c_size_t(0)
+        _check(lib().nrt_render_timings(self._h, None, 0, C.byref(n)))
+        out = (C.c_float * n.value)()
+        _check(lib().nrt_render_timings(self._h, out, n.value, None))
+        vals = [float(x) for x in out]
+        return {"kernel_ms": vals[:-1], "gather_ms": vals[-1]}
 
 
 class Builder:

@@ -7,6 +7,11 @@ usage: python scripts/ab_configs.py --reps 2 --out gpurun_out/ab.jsonl \
 Every (cfg, lib, env) combination runs `bench.py --steps S --warmup 1 --no-cpu-baseline <cfg>` as a
 child process (own timeout), repeated --reps times in alternating order; one JSON line per run
 goes to --out and a summary (best kernel ms per combination) to stdout.
+
+A run is INVALID when its kernel variant is not the one the configuration's first arm ran, or when
+a scene-specialised build failed (bench.py's "kernel_variant" then names the generic fallback): the
+arm would time another kernel than the one it names.  Invalid runs are marked ("valid": false), left
+out of the summary, and make the script exit with status 3 at the end.
 """
 import argparse
 import json
@@ -39,6 +44,8 @@ def main():
     cfgs = a.cfg or [("c5", "")]
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     best = {}
+    base_variant = {}  # cfg -> kernel_variant of its first run
+    invalid = []
     with open(a.out, "a") as fh:
         for rep in range(a.reps):
             for cname, cargs in cfgs:
@@ -58,18 +65,29 @@ def main():
                         print(f"FAIL {cname} {lname} {ename} rc={r.returncode}\n{r.stderr[-1500:]}", flush=True)
                         sys.exit(1)
                     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+                    variant = str(d.get("kernel_variant"))
+                    base = base_variant.setdefault(cname, variant)
+                    valid = variant == base and "FAILED" not in variant and "MIXED" not in variant
                     rec = {"cfg": cname, "lib": lname, "env": ename, "rep": rep, "value": d["value"],
                            "kernel_ms": d["timings_ms"]["kernel_device_only"], "frame_sha256": d["frame_sha256"],
-                           "kernel_variant": d.get("kernel_variant"), "wall_s": round(time.time() - t0, 1)}
+                           "kernel_variant": variant, "valid": valid, "wall_s": round(time.time() - t0, 1)}
                     fh.write(json.dumps(rec) + "\n")
                     fh.flush()
                     print(f"{cname:8s} {lname:8s} {ename:10s} {d['value']:10.1f} Msamples/s "
-                          f"{rec['kernel_ms']:9.3f} ms  {str(d['frame_sha256'])[:12]}", flush=True)
+                          f"{rec['kernel_ms']:9.3f} ms  {str(d['frame_sha256'])[:12]}  {variant}"
+                          + ("" if valid else "  INVALID"), flush=True)
                     key = (cname, lname, ename)
-                    best[key] = min(best.get(key, 1e30), rec["kernel_ms"])
+                    if valid:
+                        best[key] = min(best.get(key, 1e30), rec["kernel_ms"])
+                    else:
+                        invalid.append(key)
     print("best kernel ms:")
     for (c, l, e), ms in best.items():
         print(f"  {c:8s} {l:8s} {e:10s} {ms:9.3f}")
+    if invalid:
+        print(f"INVALID arms (kernel variant differs from the first arm's or a build failed): "
+              f"{sorted(set(invalid))}", flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

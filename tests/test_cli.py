@@ -73,10 +73,10 @@ def test_cli_pfm_equals_library_render(tmp_path, args, precision, rng):
 
 @pytest.mark.gpu
 def test_cli_multi_gpu_rows_equal_single_gpu(tmp_path):
-    """`--gpus N` renders rows y = g (mod N) on device g from one host thread each and un-permutes
-    them (csrc/cli.cpp); every device runs its own scene-specialised kernel or, failing that, the
-    generic one, which renders the same bits, so the frame equals the one-GPU frame without
-    NRT_JIT=require."""
+    """`--gpus N` is the library's multi-GPU render (nrt_render_opts.gpus, csrc/multi.hip): rows
+    y = g (mod N) on device g, one RCCL gather to device 0, un-permuted there; every device runs the
+    scene-specialised kernel or, failing that, the generic one, which renders the same bits, so the
+    frame equals the one-GPU frame."""
     n = nrt.device_count()
     if n < 2:
         pytest.skip("needs two GPUs")

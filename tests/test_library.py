@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nrt.lib().nrt_abi_version() == 5
+    assert nrt.lib().nrt_abi_version() == 6
 
 
 def test_camera_builder_default_and_build():

@@ -5,7 +5,10 @@ Philox pixel sums are exact.
 
   * RCCL, one process per visible GPU (skipped with fewer than two GPUs);
   * gloo, two processes sharing cuda:0 (runs on any GPU box: the shard renders of
-    several processes on the same card, the host-side gather bench.py's code uses).
+    several processes on the same card, the host-side gather bench.py's code uses);
+  * the library's own multi-GPU render in one process (nrt_render_opts.gpus, csrc/multi.hip:
+    ncclCommInitAll + one ncclGather per frame): through the RCCL code at N = 1 on any box, at
+    N >= 2 where the devices exist.
 
 The launcher (torch.distributed.run) is a child process: nothing here execs.
 """
@@ -67,14 +70,14 @@ def test_shared_gpu_processes_bitwise_identical():
         np.testing.assert_array_equal(frame, want, err_msg=f"{p}/{r}")
 
 
-def _bench(n, extra=()):
+def _bench(n, extra=(), launcher=True):
     """bench.py's own N-rank step (launched as the driver does, torch.distributed.run as a child
-    process) at a small size: its JSON line."""
+    process; launcher=False: `python bench.py --gpus N` as is) at a small size: its JSON line."""
     import json
     args = ["--gpus", str(n), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--width", "64", "--height", "37",
             "--spp", "8", *extra]
     bench = os.path.join(ROOT, "bench.py")
-    if n == 1:
+    if n == 1 or not launcher:
         cmd = [sys.executable, bench, *args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -98,6 +101,79 @@ def test_bench_multirank_step_matches_single(precision, rng):
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["value"] > 0 and two["ms_per_step"] > 0
     assert one["frame_sha256"] and two["frame_sha256"] == one["frame_sha256"]
+
+
+def test_bench_without_launcher_starts_its_ranks():
+    """`python bench.py --gpus 2 --backend gloo` with no launcher (as a driver might invoke it): bench.py
+    starts torch.distributed.run as a child process and forwards its line; the frame equals N = 1."""
+    one = _bench(1)
+    two = _bench(2, ("--backend", "gloo"), launcher=False)
+    assert two["n_gpus"] == 2 and two["multi_gpu"]["path"] == "ranks"
+    assert one["frame_sha256"] and two["frame_sha256"] == one["frame_sha256"]
+
+
+@pytest.mark.parametrize("precision,rng", VARIANTS)
+def test_library_multi_gpu_n1_through_rccl(precision, rng):
+    """nrt_render_opts.gpus = 1: the frame goes through the library's RCCL path (communicator of one,
+    ncclGather to itself, the row un-permute) and equals the single-device render bit for bit."""
+    with in_golden():
+        s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
+    want = s.render(precision=precision, rng=rng, device=0)
+    got = s.render(precision=precision, rng=rng, device=0, gpus=1)
+    np.testing.assert_array_equal(got, want)
+    t = s.render_timings()
+    assert len(t["kernel_ms"]) == 1 and t["kernel_ms"][0] > 0 and t["gather_ms"] >= 0
+
+
+def test_library_multi_gpu_device_api_pipelined():
+    """nrt_render_device with gpus = 1 into device memory, several frames enqueued back to back (the
+    two buffer sets alternate): every frame equals the single-device render."""
+    torch = pytest.importorskip("torch")
+    with in_golden():
+        s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
+    want = s.render(precision="f32", rng="philox", device=0)
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0") for _ in range(3)]
+    st = torch.cuda.current_stream(0)
+    for o in outs:
+        s.render_device(o.data_ptr(), o.numel(), precision="f32", rng="philox", device=0, stream=st.cuda_stream, gpus=1)
+    torch.cuda.synchronize(0)
+    for o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), want)
+
+
+def test_bench_library_path_n1_matches_single():
+    """bench.py --multi library (one process, the library's RCCL path) renders the frame of the default
+    single-device path."""
+    one = _bench(1)
+    lib1 = _bench(1, ("--multi", "library"))
+    assert lib1["multi_gpu"]["path"] == "library" and lib1["n_gpus"] == 1
+    assert one["frame_sha256"] and lib1["frame_sha256"] == one["frame_sha256"]
+
+
+@pytest.mark.parametrize("precision,rng", VARIANTS)
+def test_library_multi_gpu_bitwise_identical(precision, rng):
+    """nrt_render_opts.gpus = N >= 2 (every visible GPU, up to 8): the gathered, un-permuted frame equals
+    the one-GPU frame bit for bit, also for a height that leaves the last shards a row short."""
+    n = nrt.device_count()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: the library's multi-GPU render needs >= 2 devices")
+    with in_golden():
+        s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
+    want = s.render(precision=precision, rng=rng, device=0)
+    for g in sorted({2, min(n, 8)}):
+        got = s.render(precision=precision, rng=rng, device=0, gpus=g)
+        np.testing.assert_array_equal(got, want, err_msg=f"gpus={g}")
+        assert len(s.render_timings()["kernel_ms"]) == g
+
+
+def test_bench_library_multi_gpu_matches_single():
+    n = nrt.device_count()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: needs >= 2 devices")
+    one = _bench(1)
+    many = _bench(min(n, 8), launcher=False)  # no launcher, nccl: the library path
+    assert many["multi_gpu"]["path"] == "library"
+    assert many["frame_sha256"] == one["frame_sha256"]
 
 
 def test_render_on_second_device_keeps_current_device():
