@@ -190,19 +190,18 @@ def load_work(scene, w, h, spp=None):
     return same_scene
 
 
-# texel payload per format (device_scene.hpp TEXFMT_*), from the texel array's stored bytes per texel:
-# PAL16 = a 2-byte palette index per texel (+ per-band palettes: 2.0-2.8 B stored per texel; a lookup
-# reads the index from HBM and a palette word that stays in the L2), RGB8T = 3 bytes (3.2 stored with
-# the 128-B line padding), RGBA8 = 4, RGB32F = 12
-TEXEL_PAYLOAD = ((2.8, 2), (3.6, 3), (6.0, 4), (float("inf"), 12))
+# bytes a texel fetch reads as stored, per format (nrt_scene_stats.texel_formats bit 1 << f; device_scene.hpp
+# TEXFMT_*): RGB32F 12, RGBA8 4, RGB8T 3, PAL16 2 (the index; its palette word stays in the L2)
+TEXEL_FETCH_BYTES = {0: 12, 1: 4, 2: 3, 3: 2}
 
 
 def texel_payload_bytes(stats):
-    """Bytes per texel fetch as stored (2 / 3 / 4 / 12), from the texel array's bytes per texel."""
-    if not stats.get("texels"):
+    """Bytes per texel fetch as stored (2 / 3 / 4 / 12) of the scene's image textures (the largest, if
+    they use several formats); 0 without image textures."""
+    mask = stats.get("texel_formats", 0)
+    if not stats.get("texels") or not mask:
         return 0
-    per = stats["texel_bytes"] / stats["texels"]
-    return next(b for lim, b in TEXEL_PAYLOAD if per < lim)
+    return max(b for f, b in TEXEL_FETCH_BYTES.items() if mask & (1 << f))
 
 
 def work_block(wc, msamples_per_s, precision):
@@ -248,6 +247,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
                          "prints one JSON line, no GPU is touched")
+    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+                    help="1: consecutive frames' renders alternate over two HIP streams and two row buffers, so "
+                         "frame k+1's workgroups take the SIMDs frame k's last paths leave idle (each frame is "
+                         "still one full render; ms_per_step = elapsed / steps); 0: each render waits for the "
+                         "previous one")
     ap.add_argument("--kernel-only", action="store_true",
                     help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
                          "sampled over a render dispatch see the render kernel alone")
@@ -459,7 +463,9 @@ def run_library(args):
     last = host[(args.warmup + args.steps - 1) % 2].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
-    report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=tm["kernel_ms"][0], d2h_ms=d2h_ms,
+    # GPU 0's render-to-render period (the frames' renders overlap at their ends, as with --pipeline 1)
+    kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
+    report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
                       "upload": round(t_upload, 4), "jit_compile": jit_after["compile_s"],
                       "first_frame": None if first_frame is None else round(first_frame, 4)},
@@ -467,9 +473,12 @@ def run_library(args):
            kernel_variant=kernel_variant_of(jit_before, jit_after, args.steps * N),
            parallelism=f"rows interleaved over {N} GPU(s) of one process, one RCCL ncclGather to GPU 0 "
                        f"(libnrt.so nrt_render_opts.gpus)",
-           extra={"multi_gpu": {"path": "library", "kernel_ms_per_gpu": [round(x, 3) for x in tm["kernel_ms"]],
+           extra={"multi_gpu": {"path": "library", "launch_ms_per_gpu": [round(x, 3) for x in tm["kernel_ms"]],
                                 "gather_unpermute_ms": round(tm["gather_ms"], 3),
-                                "note": "HIP-event times of the last timed frame (nrt_render_timings)"}})
+                                "render_period_ms_gpu0": round(tm["period_ms"], 3),
+                                "note": "HIP-event times of the last timed frame (nrt_render_timings): each "
+                                        "device's launch begin..end (overlapping the previous frame's tail), the "
+                                        "gather + un-permute on GPU 0, GPU 0's render-to-render period"}})
 
 
 def main():
@@ -539,40 +548,49 @@ def run_ranks(args):
     rows_max = shard.rows_max(H, world)
     rows = scene.rows_selected(H, rank, world)
     assert rows == shard.rows_of(H, rank, world)
-    buf = torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream()
     lead = rank == 0
-    # double-buffered frames: render targets (N = 1) or gathered frames (N > 1, rank 0) in HBM,
-    # and pinned host frames
-    rbuf = [buf, torch.zeros_like(buf)] if world == 1 else [buf]
+    # two row buffers rendered on two streams (--pipeline 1) or one stream; N = 1: the row buffers are
+    # the frames; N > 1: rank 0 gathers into two frames.  Pinned host frames, double-buffered.
+    rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+    rstreams = [torch.cuda.Stream(device=dev) for _ in range(2)] if args.pipeline else [stream, stream]
+    freed = [None, None]  # event: rbuf[slot] consumed (copied to the host, or gathered)
     if lead:
         frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
                                           for _ in range(2)]
         host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(2)]
         copy_stream = torch.cuda.Stream(device=dev)
         copied = [None, None]
-    kev, cev = [], []
+    rend, cev = [], []
+    single = {}
 
-    def step(k, timed):
+    def step(k, timed, isolated=False):
         slot = k % 2
+        rs = rstreams[slot]
+        if freed[slot] is not None:
+            rs.wait_event(freed[slot])  # rbuf[slot] was consumed two frames ago
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        target = rbuf[slot % len(rbuf)]
-        if world == 1 and lead and copied[slot] is not None:
-            stream.wait_event(copied[slot])  # render target `slot` was copied out two frames ago
-        e0.record(stream)
-        scene.render_device(target.data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng, device=local,
-                            row_offset=rank, row_stride=world, stream=stream.cuda_stream, trace=args.trace)
-        e1.record(stream)
+        e0.record(rs)
+        scene.render_device(rbuf[slot].data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng,
+                            device=local, row_offset=rank, row_stride=world, stream=rs.cuda_stream, trace=args.trace)
+        e1.record(rs)
         if timed:
-            kev.append((e0, e1))
+            rend.append(e1)
+        if isolated:
+            single["ev"] = (e0, e1)
+        ready = e1
         if world > 1:  # the single RCCL collective + un-permute on rank 0
+            stream.wait_event(e1)
             fr = frames[slot] if lead else None
             if lead and copied[slot] is not None:
                 stream.wait_event(copied[slot])  # frame buffer `slot` was copied out two frames ago
-            shard.gather_frame(buf, H, dist, rank, world, out=fr, host=args.backend == "gloo")
-        if lead and not args.kernel_only:
+            shard.gather_frame(rbuf[slot], H, dist, rank, world, out=fr, host=args.backend == "gloo")
             ready = torch.cuda.Event()
             ready.record(stream)
+            freed[slot] = ready
+        else:
+            freed[slot] = e1
+        if lead and not args.kernel_only:
             copy_stream.wait_event(ready)
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             src = frames[slot]
@@ -581,16 +599,21 @@ def run_ranks(args):
                 host[slot].view(-1).copy_(src.view(-1)[: H * W * 3], non_blocking=True)
                 c1.record(copy_stream)
             copied[slot] = c1
+            if world == 1:
+                freed[slot] = c1
             if timed:
                 cev.append((c0, c1))
 
     first_frame = None
     for k in range(args.warmup):
-        step(k, False)
+        if k == args.warmup - 1 and k > 0:
+            torch.cuda.synchronize()  # the last warm-up frame alone on the GPU: the single-frame latency
+        step(k, False, isolated=k == args.warmup - 1 and k > 0)
         if k == 0:
             torch.cuda.synchronize()
             first_frame = time.perf_counter() - t_first0
     torch.cuda.synchronize()
+    single_ms = single["ev"][0].elapsed_time(single["ev"][1]) if single else None
     jit_before = nrt.jit_stats()  # the first render of the scene in a world mode built its kernel (warm-up)
     if world > 1:
         dist.barrier()
@@ -601,7 +624,12 @@ def run_ranks(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in kev) / max(len(kev), 1)
+    # the render's device time per frame: successive render completions (with --pipeline 1 the renders
+    # overlap at their ends, so one launch's own begin..end would count the other's tail)
+    if len(rend) >= 2:
+        kern_ms = rend[0].elapsed_time(rend[-1]) / (len(rend) - 1)
+    else:
+        kern_ms = single_ms if single_ms is not None else elapsed / max(args.steps, 1) * 1e3
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
     jit_after = nrt.jit_stats()
     specialised = jit_after["launches"] - jit_before["launches"] >= args.steps
@@ -624,7 +652,12 @@ def run_ranks(args):
                           "first_frame": None if first_frame is None else round(first_frame, 4)},
                frame_sha=frame_sha, jit_before=jit_before, jit_after=jit_after, kernel_variant=variant,
                parallelism=f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
-               extra={"multi_gpu": {"path": "ranks", "backend": args.backend}} if world > 1 else None)
+               extra=dict({"pipeline": {"on": bool(args.pipeline), "single_frame_render_ms":
+                                        None if single_ms is None else round(single_ms, 3),
+                                        "note": "kernel_ms = device time between successive render completions "
+                                                "(the steady-state time per frame's render); single_frame_render_ms "
+                                                "= one render alone on the GPU (the last warm-up frame)"}},
+                          **({"multi_gpu": {"path": "ranks", "backend": args.backend}} if world > 1 else {})))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -139,7 +139,8 @@ typedef struct {
     uint32_t world_list_ok;  /* 1: the world list resolves every such tie as the reference does
                                 (else AUTO takes the world BVH, which compares tie keys) */
     uint32_t exact_mode;     /* traversal of the f64 reference-exact kernel (NRT_EXACT_*) */
-    uint32_t reserved;
+    uint32_t texel_formats;  /* image textures' storage formats, bit 1 << f for each format f used:
+                                0 RGB32F (12 B per texel), 1 RGBA8 (4), 2 RGB8T (3), 3 PAL16 (2 + palettes) */
     /* HBM bytes of the texel array: image textures as stored (PAL16, the default for file images
      * whose bands fit: a 2-byte palette index per texel in 8 x 8 tiles plus an RGBA8 palette per
      * band; else RGB8T, 3 B per texel in 128-B tiles of 8 x 5; RGBA8 tiles; RGB32F for constructor
@@ -258,8 +259,10 @@ int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nr
  * the frame, which is written only after hip_stream's prior work.  Consecutive calls pipeline:
  * frame k+1's renders may start while frame k's last paths, gather and un-permute run. */
 /* HIP-event times (ms) of the scene's last gpus >= 1 render (waits for it): out[d] = the render
- * kernel on device first+d, d < N; out[N] = the gather + un-permute on the first device (from its
- * own render's end, so the slowest device's lag is in it).  *count = N + 1; at most n written. */
+ * launch on device first+d, d < N (begin to end; consecutive frames overlap, so this can include the
+ * previous frame's tail); out[N] = the gather + un-permute on the first device (from its own render's
+ * end, so the slowest device's lag is in it); out[N+1] = the first device's previous render end to
+ * this one's (the steady-state time per frame; 0 after one frame).  *count = N + 2; at most n written. */
 int nrt_render_timings(const nrt_scene* scene, float* out, size_t n, size_t* count);
 /* Number of rows selected by opts for an image of `height` rows. */
 uint32_t nrt_rows_selected(uint32_t height, const nrt_render_opts* opts);

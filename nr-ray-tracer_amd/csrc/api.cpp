@@ -260,9 +260,11 @@ RenderParams make_params(const nrt_camera& c, const nrt_render_opts* o, uint32_t
     // the default with spheres (the reference tests on every slot, EXACT_SIG_SLOTS); plane-only scenes
     // keep the prefiltered walk (over every slot measured slower on the Cornell box, 54.3 -> 54.9 ms at
     // spp 64).  Knob NRT_EXACT_SLOTS=0/1.
-    bool spheres = false;
+    // (the slot variants are not built for Perlin scenes, launch_impl.hpp: the flag stays 0 there)
+    bool spheres = false, perlin = false;
     for (const DPrim<double>& pr : f.prims) spheres |= pr.kind == PRIM_SPHERE;
-    p.exact_slots = spheres && f.wexact.size() <= 32 ? 1u : 0u;
+    for (const DTexture& t : f.textures) perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
+    p.exact_slots = spheres && !perlin && f.wexact.size() <= dev::EXACT_SLOTS_MAX ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_SLOTS")) p.exact_slots = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     if (const char* e = std::getenv("NRT_EXACT_PF")) p.exact_pf = std::strtol(e, nullptr, 10) != 0 ? 1u : 0u;
     // persistent lanes: fewest pixels per counter claim (0: render.hip's pick by spp); knob NRT_EXACT_CLAIM=1..64
@@ -696,7 +698,9 @@ int nrt_scene_stats_get(const nrt_scene* scene, nrt_scene_stats* out) {
         out->coplanar_pairs = f.coplanar_pairs;
         out->world_list_ok = f.world_ok && f.list_ok ? 1u : 0u;
         out->exact_mode = exact_mode(f);
-        out->reserved = 0;
+        out->texel_formats = 0;
+        for (const DTexture& t : f.textures)
+            if (t.kind == TEX_IMAGE) out->texel_formats |= 1u << t.format;
         out->texel_bytes = (uint64_t)f.texels.size() * sizeof(uint32_t);
         return NRT_OK;
     });

@@ -295,10 +295,11 @@ struct alignas(16) DMatFast {
 // word loads and a byte align per lookup (tex_rgb8_byte; heights below 65536).
 // PAL16 (default where it applies; NRT_TEX_PAL=0 keeps RGB8T): a 16-bit palette index per texel in
 // 8 x 8 tiles (one 128-byte line), then per horizontal band of 2^s rows a palette of at most 65536
-// RGBA8 words (band k's at 65536 k): images with few distinct colours per band (earth.jpg: 99 388 in
-// all, at most 62 033 per band of 256 rows; moon.jpg: 10 532) cost 2 bytes per texel instead of 3.2,
-// for a second, dependent load that mostly hits the L2 (the palettes are small).  The texture's `b`
-// holds the height | s << 16 (heights below 65536).
+// RGBA8 words, 2^p words apart (2^p = the largest band's colour count rounded up to a power of two):
+// images with few distinct colours per band (earth.jpg: 99 388 in all, at most 62 033 per band of
+// 256 rows; moon.jpg: 10 532) cost 2 bytes per texel instead of 3.2, for a second, dependent load that
+// mostly hits the L2 (the palettes are small).  Taken only where index + palettes are smaller than
+// the RGB8T layout.  The texture's `b` holds the height | s << 16 | p << 24 (heights below 65536).
 enum : uint32_t { TEXFMT_RGB32F = 0, TEXFMT_RGBA8 = 1, TEXFMT_RGB8T = 2, TEXFMT_PAL16 = 3 };
 #if defined(__HIPCC_RTC__)
 #define NRT_HD __device__
@@ -322,6 +323,10 @@ NRT_HD inline uint64_t tex_pal_index(uint32_t x, uint32_t y, uint32_t tiles_per_
 }
 NRT_HD inline uint64_t tex_pal_index_words(uint32_t w, uint32_t h) {
     return (uint64_t)((w + 7u) >> 3) * ((h + 7u) >> 3) * 32u;
+}
+// PAL16: first word of row y's band palette after the index array (b = height | s << 16 | p << 24)
+NRT_HD inline uint64_t tex_pal_band_word(uint32_t b, uint32_t y) {
+    return (uint64_t)(y >> ((b >> 16) & 31u)) << ((b >> 24) & 31u);
 }
 struct alignas(16) DTexture {
     uint32_t kind;

@@ -179,19 +179,29 @@ struct Flattener {
             if (ok) break;
             if (shift == 0 || bands >= 256u) return false;  // (too many colours per row band: RGB8T)
         }
-        d.format = TEXFMT_PAL16;
-        d.b = H | (shift << 16);
-        const size_t base = out.texels.size();
+        // palettes 2^p words apart (p: the largest band's colour count, rounded up to a power of two),
+        // and only where index + palettes take fewer bytes than RGB8T (a small or many-coloured image
+        // would otherwise grow: a 64 x 64 image with 65536-word palettes took 264 KB against 13 KB)
+        size_t most = 1;
+        for (const auto& pal : pals) most = std::max(most, pal.size());
+        uint32_t p = 0;
+        while (((size_t)1 << p) < most) ++p;
         const uint64_t iw = tex_pal_index_words(W, H);
-        out.texels.resize(base + iw + (size_t)pals.size() * 65536u, 0u);
+        const uint64_t pal_words = iw + ((uint64_t)pals.size() << p);
+        const uint64_t rgb8t_words = (uint64_t)((W + 7u) / 8u) * ((H + 4u) / 5u) * 32u;
+        if (pal_words >= rgb8t_words) return false;
+        d.format = TEXFMT_PAL16;
+        d.b = H | (shift << 16) | (p << 24);
+        const size_t base = out.texels.size();
+        out.texels.resize(base + pal_words, 0u);
         uint16_t* idx = reinterpret_cast<uint16_t*>(out.texels.data() + base);
         const uint32_t tw = (W + 7u) >> 3;
         for (uint32_t y = 0; y < H; ++y)
             for (uint32_t x = 0; x < W; ++x)
                 idx[tex_pal_index(x, y, tw)] = (uint16_t)maps[y >> shift].at(rgb[(size_t)y * W + x]);
         for (size_t k = 0; k < pals.size(); ++k)
-            std::copy(pals[k].begin(), pals[k].end(), out.texels.begin() + (std::ptrdiff_t)(base + iw + k * 65536u));
-        // (the palettes' unused tail slots are never read; the allocation keeps each band at 65536 k)
+            std::copy(pals[k].begin(), pals[k].end(), out.texels.begin() + (std::ptrdiff_t)(base + iw + (k << p)));
+        // (the palettes' unused tail slots are never read)
         return true;
     }
 

@@ -1989,7 +1989,6 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
 // stack, no divergence).  Slot order instead of walk order changes neither the candidate set's
 // outcome nor the winner (smallest exact t, ties to the higher rank: xcands_finish).  More than
 // XCAND live candidates (never seen on the reference scenes): the reference tests on every slot.
-constexpr uint32_t EXACT_SLOTS_MAX = 32;
 template <typename R, int MAXD>
 __device__ __forceinline__ bool trace_exact_slots_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 8, "exact world mode is an f64-kernel mode");
@@ -2351,7 +2350,7 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
             const uint32_t* base = sc.texels + t.offset;
             const uint64_t i = tex_pal_index(x, y, (t.a + 7u) >> 3);
             const uint32_t pi = (base[i >> 1] >> ((uint32_t)(i & 1u) * 16u)) & 0xFFFFu;
-            const uint32_t w = base[tex_pal_index_words(t.a, th) + ((uint64_t)(y >> (t.b >> 16)) << 16) + pi];
+            const uint32_t w = base[tex_pal_index_words(t.a, th) + tex_pal_band_word(t.b, y) + pi];
             return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
         }
         if (t.kind == TEX_SOLID) return ld3d<R>(t.color);
@@ -2379,7 +2378,7 @@ __device__ V<R> tex_color(const DSceneView<R>& sc, uint32_t tid, R u, R v, V<R> 
                 const uint32_t* base = sc.texels + t.offset;
                 const uint64_t i = tex_pal_index(x, y, (t.a + 7u) >> 3);
                 const uint32_t pi = (base[i >> 1] >> ((uint32_t)(i & 1u) * 16u)) & 0xFFFFu;
-                const uint32_t w = base[tex_pal_index_words(t.a, th) + ((uint64_t)(y >> (t.b >> 16)) << 16) + pi];
+                const uint32_t w = base[tex_pal_index_words(t.a, th) + tex_pal_band_word(t.b, y) + pi];
                 return mk((R)unorm8(w & 0xFFu), (R)unorm8((w >> 8) & 0xFFu), (R)unorm8((w >> 16) & 0xFFu));
             }
             if ((NRT_TEX_FORMATS & 4) && t.format == TEXFMT_RGB8T) {
@@ -2567,7 +2566,8 @@ template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p
         // f64: scalar loads from the kernel arguments at the use (the offset laundered, so the loads
         // are not hoisted out of the loop): seven f64 vectors held live through the loop spilled the
         // earth scene's exact kernel to scratch (42 registers' worth; the camera ray and the
-        // background are the only readers).  RenderParams is the kernel's first argument.
+        // background are the only readers).  RenderParams is the kernel's first argument (kernarg
+        // offset 0; see render_kernel).
         (void)p;
         (void)d;
         constexpr uint32_t off[7] = {
@@ -2596,6 +2596,9 @@ struct MatV {
 template <bool COMPACT> struct StackEntry { using type = int32_t; };
 template <> struct StackEntry<true> { using type = uint16_t; };
 
+// RenderParams must stay the FIRST by-value parameter (kernarg offset 0): the f64 cam3 reads the camera
+// vectors straight from the kernarg segment at offsetof(RenderParams, ...) (the exact earth / C5 parity
+// cases, whose cameras are off the origin, catch a reordering).
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS = 0, class SIG = NoSig>
 __global__ void __launch_bounds__(BLOCK, (min_waves_per_simd<R, G, MAXD, SIG>(KFLAGS)))
 render_kernel(const RenderParams p, const DSceneView<R> gsc) {

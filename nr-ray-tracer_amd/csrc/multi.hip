@@ -19,7 +19,8 @@
 // is in the process, else /opt/rocm's), so libnrt.so loads and renders on one device without it.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>  // types only: the functions come from dlopen below
+#include <rccl/rccl.h>
+#include <unistd.h>  // types only: the functions come from dlopen below
 
 #include <algorithm>
 #include <cstdio>
@@ -229,7 +230,19 @@ MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes) {
             }
         }
         m->comms.assign((size_t)m->n, nullptr);
-        ncheck(r.init_all(m->comms.data(), m->n, devlist.data()), "ncclCommInitAll");
+        // RCCL prints a version banner on stdout at its first init; a library keeps the caller's
+        // stdout clean (bench.py's one JSON line, a CLI writing an image to stdout): the banner goes
+        // to stderr
+        std::fflush(stdout);
+        const int saved = ::dup(1);
+        if (saved >= 0) (void)::dup2(2, 1);
+        const ncclResult_t ir = r.init_all(m->comms.data(), m->n, devlist.data());
+        std::fflush(stdout);
+        if (saved >= 0) {
+            (void)::dup2(saved, 1);
+            ::close(saved);
+        }
+        ncheck(ir, "ncclCommInitAll");
     } catch (...) {
         gpu_multi_free(m);
         throw;
@@ -354,20 +367,23 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
     std::lock_guard<std::mutex> lock(m->mu);
     if (m->last < 0) throw std::invalid_argument("no multi-GPU render of this scene yet");
     const int s = m->last;
-    for (int d = 0; d <= m->n; ++d) {
+    for (int d = 0; d <= m->n + 1; ++d) {
         float ms = 0.0f;
         if (d < m->n) {
             Guard g(m->first + d);
             hcheck(hipEventSynchronize(m->dev[(size_t)d].t1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->dev[(size_t)d].t0[s], m->dev[(size_t)d].t1[s]), "hipEventElapsedTime");
-        } else {
+        } else if (d == m->n) {
             Guard g(m->first);
             hcheck(hipEventSynchronize(m->g1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->g0[s], m->g1[s]), "hipEventElapsedTime");
+        } else if (m->frames >= 2) {  // first device: the previous frame's render end -> this one's
+            Guard g(m->first);
+            hcheck(hipEventElapsedTime(&ms, m->dev[0].t1[1 - s], m->dev[0].t1[s]), "hipEventElapsedTime");
         }
         if ((size_t)d < n) out[d] = ms;
     }
-    return (size_t)m->n + 1;
+    return (size_t)m->n + 2;
 }
 
 }  // namespace nrt

@@ -23,6 +23,9 @@ namespace dev {
 // whose materials all have solid colours, KF_PLANES = f64 kernel, no spheres, KF_TEXPAL = every
 // texture is a solid colour or a PAL16 image (scene-specialised kernels only) (kernel.hpp).
 constexpr int KF_PROF = 1, KF_PERLIN = 2, KF_FLAT = 4, KF_PLANES = 8, KF_TEXPAL = 16;
+// Exact kernel, small scenes: at most this many slots of the culling tree are tested in slot order
+// instead of walked (EXACT_SIG_SLOTS / EXACT_SIG_SLOTS_PF; host default and launcher share it)
+constexpr uint32_t EXACT_SLOTS_MAX = 32;
 }  // namespace dev
 
 struct RenderParams {

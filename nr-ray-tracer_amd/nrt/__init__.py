@@ -70,7 +70,7 @@ class _SceneStats(C.Structure):
                 ("materials", C.c_uint64), ("textures", C.c_uint64), ("texels", C.c_uint64), ("trees", C.c_uint32),
                 ("max_instance_depth", C.c_uint32), ("device_bytes", C.c_uint64), ("world_prims", C.c_uint64),
                 ("coplanar_pairs", C.c_uint32), ("world_list_ok", C.c_uint32), ("exact_mode", C.c_uint32),
-                ("reserved", C.c_uint32), ("texel_bytes", C.c_uint64)]
+                ("texel_formats", C.c_uint32), ("texel_bytes", C.c_uint64)]
 
 
 PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64)
@@ -459,14 +459,14 @@ class Scene:
 
 
     def render_timings(self) -> dict:
-        """HIP-event times of the last gpus >= 1 render (nrt_render_timings): per-device render kernel ms
-        and the gather + un-permute ms on the first device."""
+        """HIP-event times of the last gpus >= 1 render (nrt_render_timings): per-device render launch ms,
+        the gather + un-permute ms on the first device, and the first device's render-to-render period."""
         n = C.c_size_t(0)
         _check(lib().nrt_render_timings(self._h, None, 0, C.byref(n)))
         out = (C.c_float * n.value)()
         _check(lib().nrt_render_timings(self._h, out, n.value, None))
         vals = [float(x) for x in out]
-        return {"kernel_ms": vals[:-1], "gather_ms": vals[-1]}
+        return {"kernel_ms": vals[:-2], "gather_ms": vals[-2], "period_ms": vals[-1]}
 
 
 class Builder:

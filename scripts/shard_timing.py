@@ -7,7 +7,10 @@ loss is the longest paths' serial bounces).
 Each N is timed two ways: `shard_ms` brackets one launch with events after a synchronize (the host's
 launch work, occupancy queries and hipModuleLaunchKernel, counts when the GPU waits for it), and
 `shard_ms_queued` the same launch enqueued behind a previous one, so the GPU is still busy while the
-host prepares it (as in bench.py's double-buffered loop): the kernel alone.
+host prepares it (as in bench.py's double-buffered loop): the kernel alone.  `shard_ms_pipelined`:
+K launches alternating over two streams and two buffers (the library's multi-GPU render does this,
+csrc/multi.hip), total device time / K: launch k+1's workgroups take the SIMDs launch k's last paths
+leave idle, so the per-launch tail overlaps the next launch's start.
 """
 import json
 import os
@@ -27,7 +30,10 @@ s = nrt.Scene.load(scene, nrt.CameraConfig(width=W, height=H, samples_per_pixel=
 s.upload(0)
 buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
 stream = torch.cuda.current_stream()
-res, resq = {}, {}
+buf2 = torch.zeros_like(buf)
+stream2 = torch.cuda.Stream(device="cuda:0")
+res, resq, resp = {}, {}, {}
+K = 8
 ns = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1, 2, 4, 8]
 for n in ns:
     rows = (H + n - 1) // n
@@ -52,9 +58,27 @@ for n in ns:
             queued.append(q0.elapsed_time(q1))
     res[n] = sum(times) / len(times)
     resq[n] = sum(queued) / len(queued)
-base, baseq = res[ns[0]] * ns[0], resq[ns[0]] * ns[0]
+    piped = []
+    for it in range(3):
+        torch.cuda.synchronize()
+        p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        p0.record(stream)
+        stream2.wait_event(p0)
+        done2 = torch.cuda.Event()
+        for k in range(K):
+            st, b = (stream, buf) if k % 2 == 0 else (stream2, buf2)
+            s.render_device(b.data_ptr(), rows * W * 3, row_offset=0, row_stride=n, stream=st.cuda_stream)
+        done2.record(stream2)
+        stream.wait_event(done2)
+        p1.record(stream)
+        torch.cuda.synchronize()
+        piped.append(p0.elapsed_time(p1) / K)
+    resp[n] = min(piped)
+base, baseq, basep = res[ns[0]] * ns[0], resq[ns[0]] * ns[0], resp[ns[0]] * ns[0]
 out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(base / (n * t), 4),
-                  "shard_ms_queued": round(resq[n], 3), "efficiency_queued": round(baseq / (n * resq[n]), 4)}
+                  "shard_ms_queued": round(resq[n], 3), "efficiency_queued": round(baseq / (n * resq[n]), 4),
+                  "shard_ms_pipelined": round(resp[n], 3), "efficiency_pipelined": round(basep / (n * resp[n]), 4),
+                  "efficiency_pipelined_vs_unpipelined_N1": round(base / (n * resp[n]), 4)}
        for n, t in res.items()}
 out["env"] = {k: v for k, v in os.environ.items() if k.startswith(("NRT_", "SHARD_"))}
 print(json.dumps(out))

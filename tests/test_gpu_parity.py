@@ -32,7 +32,8 @@ CASES_F64 = [
     ("scenes/cornell-box-scene.json", 17, 13, 1, None),   # spp = 1: no jitter draws (Q3)
     ("scenes/cornell-box-scene.json", 20, 20, 3, 2),      # bounce cap 2 (Q6)
     ("scenes/utah-teapot-scene.json", 32, 24, 2, None),   # 7520 triangles, deep BLAS (generated model, Q16)
-    ("scenes/earth.toml", 48, 27, 2, None),               # image textures (JPEG), r = 1000 ground sphere
+    ("scenes/earth.toml", 48, 27, 2, None),               # image textures (JPEG), r = 1000 ground sphere; camera
+    # off the origin: pins the f64 kernel reading the camera from the kernarg segment (kernel.hpp cam3)
     ("scenes/noise.toml", 40, 30, 2, None),               # Perlin Noise + Marble textures (parity unpinned)
     ("scenes/simple-lights.toml", 40, 30, 2, None),       # Marble + emissive quad / sphere
     ("scenes/triangles.toml", 40, 30, 4, None),           # legacy index schema (Q14)

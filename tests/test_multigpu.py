@@ -122,7 +122,7 @@ def test_library_multi_gpu_n1_through_rccl(precision, rng):
     got = s.render(precision=precision, rng=rng, device=0, gpus=1)
     np.testing.assert_array_equal(got, want)
     t = s.render_timings()
-    assert len(t["kernel_ms"]) == 1 and t["kernel_ms"][0] > 0 and t["gather_ms"] >= 0
+    assert len(t["kernel_ms"]) == 1 and t["kernel_ms"][0] > 0 and t["gather_ms"] >= 0 and t["period_ms"] == 0
 
 
 def test_library_multi_gpu_device_api_pipelined():

@@ -50,11 +50,13 @@ def test_bench_work_block():
     other = bench.load_work(bench.DEFAULT_SCENE, 100, 100)
     assert other["counted_at"] in ("512x512", "1024x1024") and other["scene"] == bench.DEFAULT_SCENE
     assert bench.load_work("scenes/quads.toml", 100, 100) is None
-    # SURVEY §8(d) texel bytes at the bytes per texel as stored: 3-byte texels in 128-B lines of 40
-    assert bench.texel_payload_bytes({"texels": 40, "texel_bytes": 128}) == 3
-    assert bench.texel_payload_bytes({"texels": 4194304, "texel_bytes": 9437184}) == 2  # PAL16, earth.toml
-    assert bench.texel_payload_bytes({"texels": 32, "texel_bytes": 128}) == 4
-    assert bench.texel_payload_bytes({"texels": 4, "texel_bytes": 48}) == 12
-    assert bench.texel_payload_bytes({"texels": 0, "texel_bytes": 0}) == 0
+    # SURVEY §8(d) texel bytes at the bytes per texel as stored, by the formats the scene's images use
+    # (nrt_scene_stats.texel_formats: bit 1 << f, f = RGB32F 0, RGBA8 1, RGB8T 2, PAL16 3)
+    assert bench.texel_payload_bytes({"texels": 40, "texel_bytes": 128, "texel_formats": 1 << 2}) == 3
+    assert bench.texel_payload_bytes({"texels": 4194304, "texel_bytes": 9437184, "texel_formats": 1 << 3}) == 2
+    assert bench.texel_payload_bytes({"texels": 32, "texel_bytes": 128, "texel_formats": 1 << 1}) == 4
+    assert bench.texel_payload_bytes({"texels": 4, "texel_bytes": 48, "texel_formats": 1 << 0}) == 12
+    assert bench.texel_payload_bytes({"texels": 8, "texel_bytes": 60, "texel_formats": (1 << 3) | (1 << 2)}) == 3
+    assert bench.texel_payload_bytes({"texels": 0, "texel_bytes": 0, "texel_formats": 0}) == 0
     c3 = bench.load_work("scenes/earth.toml", 1920, 1080)
     assert c3["name"] == "C3" and c3["per_sample"]["texel_fetches"] > 0.2
