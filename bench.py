@@ -26,7 +26,7 @@ Two ways to run N > 1, both the same frame bit for bit (frame_sha256 on the line
 
 The frame is fixed as N grows, so scaling is "strong".
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]      # N > 1: the library's multi-GPU render
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  `roofline` prices the render kernel against the

@@ -30,7 +30,10 @@
 namespace nrt {
 namespace dev {
 
-constexpr int BLOCK = 256;
+#ifndef NRT_BLOCK
+#define NRT_BLOCK 256  // threads per workgroup (a multiple of 64)
+#endif
+constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_SPECULATIVE
 #define NRT_SPECULATIVE 1  // world-BVH rounds: lanes holding a leaf keep descending (Aila & Laine)
 #endif

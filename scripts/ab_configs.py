@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--lib", action="append", type=kv, default=[])
     ap.add_argument("--env", action="append", type=kv, default=[])
     ap.add_argument("--cfg", action="append", type=kv, default=[])
+    ap.add_argument("--arm", action="append", type=kv, default=[],
+                    help="NAME=LIBPATH::ENV ... : one (library, environment) pair, instead of the --lib x --env product")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--timeout", type=int, default=120)
@@ -50,6 +52,11 @@ def main():
         for rep in range(a.reps):
             for cname, cargs in cfgs:
                 combos = [(l, e) for l in libs for e in envs]
+                if a.arm:
+                    combos = []
+                    for name, spec in a.arm:
+                        lp, _, es = spec.partition("::")
+                        combos.append(((name, lp or libs[0][1]), ("-", es)))
                 if rep % 2:
                     combos.reverse()
                 for (lname, lpath), (ename, estr) in combos:

@@ -56,12 +56,28 @@ def main():
         e["variant"] = v
         e.update({k: d.get(k) for k in KEEP})
         e["bench_kernel_ms"] = bench["roofline"]["kernel_ms"]
+        tp = os.path.join(src, "trace_period.json")  # scripts/trace_period.py (pipelined runs)
+        if os.path.exists(tp):
+            shutil.copy(tp, os.path.join(prof, f"{a.name}_{v}_trace_period.json"))
+            with open(tp) as fh:
+                per = next(iter(json.load(fh).values()), {})
+            e["steady_period_ns"] = per.get("steady_period_ns")
+            e["mean_overlap_ns"] = per.get("mean_overlap_ns")
         e["source"] = (f"profiles/{a.name}_{v}_pmc.json + {a.name}_{v}_kernel_stats.csv (rocprofv3 --kernel-trace "
                        f"--stats, then --pmc, one counter group per pass; FETCH_SIZE x2 per MI355X_MICROARCH.md; "
                        f"valu_issue_frac in 2-cycle wave64 slots)")
         entries.append(e)
-    with open(os.path.join(prof, "pmc_summary.json"), "w") as fh:
-        fh.write(json.dumps({"round": a.name, "entries": entries}, indent=1) + "\n")
+    # merge: entries of other configurations (earlier rounds' profiles) stay until re-profiled
+    summ = os.path.join(prof, "pmc_summary.json")
+    old = []
+    if os.path.exists(summ):
+        with open(summ) as fh:
+            old = json.load(fh).get("entries", [])
+    keyof = lambda e: tuple(e.get(k) for k in KEY + ("n_gpus",))  # noqa: E731
+    new_keys = {keyof(e) for e in entries}
+    merged = [e for e in old if keyof(e) not in new_keys] + entries
+    with open(summ, "w") as fh:
+        fh.write(json.dumps({"round": a.name, "entries": merged}, indent=1) + "\n")
     print(json.dumps(entries, indent=1))
 
 

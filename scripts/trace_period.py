@@ -1,0 +1,57 @@
+"""Render-kernel timing from a rocprofv3 kernel trace (run_kernel_trace.csv), for pipelined runs.
+
+usage: python scripts/trace_period.py <rocprofv3 -d dir or run_kernel_trace.csv> [--json out.json]
+
+With bench.py --pipeline 1 consecutive frames' render launches overlap at their ends (frame k+1's
+workgroups start on the SIMDs frame k's last paths leave idle), so one dispatch's begin..end also
+counts the other frame's tail and rocprofv3's AverageNs exceeds the time a frame costs.  This prints,
+per render-kernel name: dispatches, the mean begin..end duration (what --stats averages), the
+steady-state period = (last end - first end) / (n - 1) over the dispatches after the first two
+(warm-up / module load), which is what bench.py's roofline.kernel_ms measures with HIP events, and
+the overlap between consecutive dispatches.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("--json")
+    ap.add_argument("--skip", type=int, default=2, help="leading dispatches left out of the period (warm-up)")
+    a = ap.parse_args()
+    path = a.src
+    if os.path.isdir(path):
+        path = next(iter(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)), None)
+        if path is None:
+            sys.exit("no *kernel_trace.csv")
+    rows = {}
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            name = r["Kernel_Name"]
+            if "render_kernel" not in name:
+                continue
+            rows.setdefault(name, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    out = {}
+    for name, d in rows.items():
+        d.sort(key=lambda x: x[1])
+        dur = [e - s for s, e in d]
+        steady = d[a.skip:] if len(d) > a.skip + 1 else d
+        period = (steady[-1][1] - steady[0][1]) / (len(steady) - 1) if len(steady) > 1 else None
+        overlap = [max(0, d[i][1] - d[i + 1][0]) for i in range(len(d) - 1)]
+        out[name] = {"dispatches": len(d), "mean_duration_ns": sum(dur) / len(dur),
+                     "steady_period_ns": period, "steady_dispatches": len(steady),
+                     "mean_overlap_ns": sum(overlap) / len(overlap) if overlap else 0.0,
+                     "source": os.path.relpath(path)}
+    print(json.dumps(out, indent=1))
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
