@@ -5,7 +5,7 @@ tag=${1:-cfg}
 mkdir -p gpurun_out
 run() {  # name, args...
   local name=$1; shift
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${tag}_$name.json 2> gpurun_out/${tag}_$name.err || { echo "bench $name failed rc=$?"; tail -3 gpurun_out/${tag}_$name.err; return 1; }
+  timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/${tag}_$name.json 2> gpurun_out/${tag}_$name.err || { echo "bench $name failed rc=$?"; tail -3 gpurun_out/${tag}_$name.err; return 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], 'Msamples/s', d['roofline']['kernel_ms'], 'ms', d['config'].get('trace'), d['config'].get('world_prims'))" gpurun_out/${tag}_$name.json $name
 }
 run c2_f32 --scene scenes/cornell-box-scene.json --width 512 --height 512 --spp 64 && \
