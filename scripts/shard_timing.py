@@ -8,7 +8,7 @@ Each N is timed two ways: `shard_ms` brackets one launch with events after a syn
 launch work, occupancy queries and hipModuleLaunchKernel, counts when the GPU waits for it), and
 `shard_ms_queued` the same launch enqueued behind a previous one, so the GPU is still busy while the
 host prepares it (as in bench.py's double-buffered loop): the kernel alone.  `shard_ms_pipelined`:
-K launches alternating over two streams and two buffers (the library's multi-GPU render does this,
+K launches alternating over SHARD_STREAMS (default 2) streams and buffers (the library's multi-GPU render does this,
 csrc/multi.hip), total device time / K: launch k+1's workgroups take the SIMDs launch k's last paths
 leave idle, so the per-launch tail overlaps the next launch's start.
 """
@@ -30,8 +30,9 @@ s = nrt.Scene.load(scene, nrt.CameraConfig(width=W, height=H, samples_per_pixel=
 s.upload(0)
 buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
 stream = torch.cuda.current_stream()
-buf2 = torch.zeros_like(buf)
-stream2 = torch.cuda.Stream(device="cuda:0")
+NSTREAMS = int(os.environ.get("SHARD_STREAMS", "2"))  # pipelined mode: launches in flight
+pbufs = [buf] + [torch.zeros_like(buf) for _ in range(NSTREAMS - 1)]
+pstreams = [stream] + [torch.cuda.Stream(device="cuda:0") for _ in range(NSTREAMS - 1)]
 res, resq, resp = {}, {}, {}
 K = 8
 ns = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1, 2, 4, 8]
@@ -63,13 +64,15 @@ for n in ns:
         torch.cuda.synchronize()
         p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         p0.record(stream)
-        stream2.wait_event(p0)
-        done2 = torch.cuda.Event()
+        for st in pstreams[1:]:
+            st.wait_event(p0)
         for k in range(K):
-            st, b = (stream, buf) if k % 2 == 0 else (stream2, buf2)
+            st, b = pstreams[k % NSTREAMS], pbufs[k % NSTREAMS]
             s.render_device(b.data_ptr(), rows * W * 3, row_offset=0, row_stride=n, stream=st.cuda_stream)
-        done2.record(stream2)
-        stream.wait_event(done2)
+        for st in pstreams[1:]:
+            done = torch.cuda.Event()
+            done.record(st)
+            stream.wait_event(done)
         p1.record(stream)
         torch.cuda.synchronize()
         piped.append(p0.elapsed_time(p1) / K)
