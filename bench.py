@@ -247,11 +247,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
                          "prints one JSON line, no GPU is touched")
-    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
-                    help="1: consecutive frames' renders alternate over two HIP streams and two row buffers, so "
-                         "frame k+1's workgroups take the SIMDs frame k's last paths leave idle (each frame is "
-                         "still one full render; ms_per_step = elapsed / steps); 0: each render waits for the "
-                         "previous one")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="frames whose renders may be in flight at once: consecutive renders rotate over this many "
+                         "HIP streams and row buffers, so frame k+1's workgroups take the SIMDs frame k's last paths "
+                         "leave idle (each frame is still one full render; ms_per_step = elapsed / steps); 1 (or 0): "
+                         "each render waits for the previous one")
     ap.add_argument("--kernel-only", action="store_true",
                     help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
                          "sampled over a render dispatch see the render kernel alone")
@@ -419,16 +419,17 @@ def run_library(args):
         scene.upload(d)
     t_upload = time.perf_counter() - t0
     stream = torch.cuda.current_stream()
-    frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
-    host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(2)]
+    D = max(1, args.pipeline)  # device / pinned host frames (the library keeps its own buffer sets)
+    frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(D)]
+    host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(D)]
     copy_stream = torch.cuda.Stream(device=dev)
-    copied = [None, None]
+    copied = [None] * D
     cev = []
 
     def step(k, timed):
-        slot = k % 2
+        slot = k % D
         if copied[slot] is not None:
-            stream.wait_event(copied[slot])  # frame `slot` was copied out two frames ago
+            stream.wait_event(copied[slot])  # frame `slot` was copied out D frames ago
         scene.render_device(frames[slot].data_ptr(), H * W * 3, precision=args.precision, rng=args.rng, device=0,
                             stream=stream.cuda_stream, trace=args.trace, gpus=N)
         if not args.kernel_only:
@@ -460,10 +461,10 @@ def run_library(args):
     tm = scene.render_timings()  # the last timed frame's per-device kernel and gather times
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
     jit_after = nrt.jit_stats()
-    last = host[(args.warmup + args.steps - 1) % 2].numpy()
+    last = host[(args.warmup + args.steps - 1) % D].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
-    # GPU 0's render-to-render period (the frames' renders overlap at their ends, as with --pipeline 1)
+    # GPU 0's render-to-render period (the frames' renders overlap at their ends, as with --pipeline > 1)
     kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
     report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
@@ -550,25 +551,26 @@ def run_ranks(args):
     assert rows == shard.rows_of(H, rank, world)
     stream = torch.cuda.current_stream()
     lead = rank == 0
-    # two row buffers rendered on two streams (--pipeline 1) or one stream; N = 1: the row buffers are
-    # the frames; N > 1: rank 0 gathers into two frames.  Pinned host frames, double-buffered.
-    rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(2)]
-    rstreams = [torch.cuda.Stream(device=dev) for _ in range(2)] if args.pipeline else [stream, stream]
-    freed = [None, None]  # event: rbuf[slot] consumed (copied to the host, or gathered)
+    # D = --pipeline row buffers rendered on D streams (D = 1: one stream); N = 1: the row buffers are
+    # the frames; N > 1: rank 0 gathers into D frames.  Pinned host frames, one per buffer.
+    D = max(1, args.pipeline)
+    rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(D)]
+    rstreams = [torch.cuda.Stream(device=dev) for _ in range(D)] if D > 1 else [stream]
+    freed = [None] * D  # event: rbuf[slot] consumed (copied to the host, or gathered)
     if lead:
         frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
-                                          for _ in range(2)]
-        host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(2)]
+                                          for _ in range(D)]
+        host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(D)]
         copy_stream = torch.cuda.Stream(device=dev)
-        copied = [None, None]
+        copied = [None] * D
     rend, cev = [], []
     single = {}
 
     def step(k, timed, isolated=False):
-        slot = k % 2
+        slot = k % D
         rs = rstreams[slot]
         if freed[slot] is not None:
-            rs.wait_event(freed[slot])  # rbuf[slot] was consumed two frames ago
+            rs.wait_event(freed[slot])  # rbuf[slot] was consumed D frames ago
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(rs)
         scene.render_device(rbuf[slot].data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng,
@@ -583,7 +585,7 @@ def run_ranks(args):
             stream.wait_event(e1)
             fr = frames[slot] if lead else None
             if lead and copied[slot] is not None:
-                stream.wait_event(copied[slot])  # frame buffer `slot` was copied out two frames ago
+                stream.wait_event(copied[slot])  # frame buffer `slot` was copied out D frames ago
             shard.gather_frame(rbuf[slot], H, dist, rank, world, out=fr, host=args.backend == "gloo")
             ready = torch.cuda.Event()
             ready.record(stream)
@@ -624,7 +626,7 @@ def run_ranks(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # the render's device time per frame: successive render completions (with --pipeline 1 the renders
+    # the render's device time per frame: successive render completions (with --pipeline > 1 the renders
     # overlap at their ends, so one launch's own begin..end would count the other's tail)
     if len(rend) >= 2:
         kern_ms = rend[0].elapsed_time(rend[-1]) / (len(rend) - 1)
@@ -644,7 +646,7 @@ def run_ranks(args):
         mixed = float(t[2]) != -float(t[3])
     variant = kernel_variant_of(jit_before, jit_after, args.steps, mixed)
     if lead:
-        last = host[(args.warmup + args.steps - 1) % 2].numpy()
+        last = host[(args.warmup + args.steps - 1) % D].numpy()
         frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
         report(args, nrt, scene, n_gpus=world, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
                timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
@@ -652,7 +654,7 @@ def run_ranks(args):
                           "first_frame": None if first_frame is None else round(first_frame, 4)},
                frame_sha=frame_sha, jit_before=jit_before, jit_after=jit_after, kernel_variant=variant,
                parallelism=f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
-               extra=dict({"pipeline": {"on": bool(args.pipeline), "single_frame_render_ms":
+               extra=dict({"pipeline": {"frames_in_flight": D, "single_frame_render_ms":
                                         None if single_ms is None else round(single_ms, 3),
                                         "note": "kernel_ms = device time between successive render completions "
                                                 "(the steady-state time per frame's render); single_frame_render_ms "

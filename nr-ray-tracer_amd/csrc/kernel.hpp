@@ -66,6 +66,12 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_SPHERE_REPROJ
 #define NRT_SPHERE_REPROJ 1  // f32-tested spheres: hit points put back on the surface (make_record_world)
 #endif
+#ifndef NRT_WL_RELOAD
+#define NRT_WL_RELOAD 0  // world list: the unit records' scalar loads per query (not hoisted out of the loop)
+#endif
+#ifndef NRT_CAM_RELOAD
+#define NRT_CAM_RELOAD 0  // f32 camera vectors: scalar loads from the kernel arguments at the use
+#endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 // ChaCha8 (persistent-lane) kernels' dynamic LDS before the stack and the staged scene: the ring,
 // then each lane's f64 pixel sums (kept in LDS, not registers: the earth scene's exact kernel spilled
@@ -1016,7 +1022,15 @@ __device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float
 template <typename R, int MAXD, bool FLAT = false, class SIG = NoSig>
 __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R>& ray, HitMin<R, MAXD>& hm) {
     static_assert(sizeof(R) == 4, "world-space mode is an f32-kernel mode");
+#if NRT_WL_RELOAD
+    // the records' scalar loads stay inside the loop (the base laundered per query): loop-invariant
+    // records no longer hold ~30 SGPRs for the whole kernel (occupancy experiments)
+    uint64_t wpi = (uint64_t)sc.wprims;
+    asm volatile("" : "+s"(wpi));
+    const ConstPrimWorld<float> wp = (ConstPrimWorld<float>)wpi;
+#else
     const ConstPrimWorld<float> wp = (ConstPrimWorld<float>)sc.wprims;
+#endif
     const ConstU32 runs = (ConstU32)sc.wruns;
     float t_best = INFINITY;
     int32_t best = -1;
@@ -2564,7 +2578,20 @@ static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole 
 // (kernel arguments stay in SGPRs), the f64 kernel the double.
 template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
     if constexpr (sizeof(R) == 4) {
+#if NRT_CAM_RELOAD
+        // scalar loads from the kernel arguments at the use (offset laundered: not hoisted), as the
+        // f64 branch below: 21 SGPRs less held through the loop (occupancy experiments)
+        (void)p;
+        (void)d;
+        uint32_t o = (uint32_t)__builtin_offsetof(RenderParams, camf) + (uint32_t)q * 12u;
+        asm volatile("" : "+s"(o));
+        typedef const __attribute__((address_space(4))) unsigned char* KArgF;
+        const KArgF base = (KArgF)__builtin_amdgcn_kernarg_segment_ptr();
+        const __attribute__((address_space(4))) float* fp = (const __attribute__((address_space(4))) float*)(base + o);
+        return mk(fp[0], fp[1], fp[2]);
+#else
         return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
+#endif
     } else {
         // f64: scalar loads from the kernel arguments at the use (the offset laundered, so the loads
         // are not hoisted out of the loop): seven f64 vectors held live through the loop spilled the

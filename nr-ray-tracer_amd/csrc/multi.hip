@@ -5,12 +5,14 @@
 // whole machine (rayon's global pool, lib/camera.rs:315-316); this is that call for a node of
 // MI355Xs.  nrt_render / nrt_render_device with nrt_render_opts.gpus = N reach it.
 //
-// Layout per context (one per (first device, N) of a scene), double-buffered so frame k+1's
+// Layout per context (one per (first device, N) of a scene), PIPE buffer sets so frame k+1's
 // renders can start while frame k's gather and un-permute run (and while frame k's slowest
-// paths finish: the two render streams of a device overlap one frame's tail with the next
-// frame's start):
-//   device d:  rows[2]   (rows_max x W x 3 f32 each), render streams rs[2], one comm stream cs
-//   device 0:  staging[2] (N x rows_max x W x 3 f32), the gather's receive buffers
+// paths finish: the render streams of a device overlap one frame's tail with the next frame's
+// start).  Two sets: three in flight measured N = 8 shards 0.931 -> 0.935-0.940 of linear but the
+// whole C5 step 1-2 % slower (more streams than the process's 4 hardware queues: the host copy then
+// shares a queue with a render):
+//   device d:  rows[PIPE]   (rows_max x W x 3 f32 each), render streams rs[PIPE], one comm stream cs
+//   device 0:  staging[PIPE] (N x rows_max x W x 3 f32), the gather's receive buffers
 // The comm stream carries every gather of its device in issue order (RCCL requires the same
 // order on every rank; one stream per communicator keeps it), after an event of the frame's
 // render stream.  One host thread enqueues all devices: every call here is asynchronous.
@@ -112,6 +114,8 @@ __global__ void __launch_bounds__(256) unpermute_rows(const float* __restrict__ 
     }
 }
 
+constexpr int PIPE = 2;  // buffer sets (frames in flight)
+
 }  // namespace
 
 struct MultiRender {
@@ -119,18 +123,18 @@ struct MultiRender {
     std::vector<DeviceScene*> scenes;  // scenes[d] lives on device first + d
     std::vector<ncclComm_t> comms;
     struct Dev {
-        hipStream_t rs[2] = {nullptr, nullptr};  // render streams (frames alternate)
-        hipStream_t cs = nullptr;                // comm stream (every gather, in issue order)
-        float* rows[2] = {nullptr, nullptr};
-        hipEvent_t rendered[2] = {nullptr, nullptr}, gathered[2] = {nullptr, nullptr};
-        hipEvent_t t0[2] = {nullptr, nullptr}, t1[2] = {nullptr, nullptr};  // render kernel timing
+        hipStream_t rs[PIPE] = {};  // render streams (frames rotate)
+        hipStream_t cs = nullptr;   // comm stream (every gather, in issue order)
+        float* rows[PIPE] = {};
+        hipEvent_t rendered[PIPE] = {}, gathered[PIPE] = {};
+        hipEvent_t t0[PIPE] = {}, t1[PIPE] = {};  // render kernel timing
     };
     std::vector<Dev> dev;
-    float* staging[2] = {nullptr, nullptr};
+    float* staging[PIPE] = {};
     float* frame = nullptr;  // nrt_render's device frame on the first device
     hipStream_t host_stream = nullptr;
-    hipEvent_t in_ev[2] = {nullptr, nullptr}, done_ev[2] = {nullptr, nullptr};
-    hipEvent_t g0[2] = {nullptr, nullptr}, g1[2] = {nullptr, nullptr};  // gather + un-permute timing
+    hipEvent_t in_ev[PIPE] = {}, done_ev[PIPE] = {};
+    hipEvent_t g0[PIPE] = {}, g1[PIPE] = {};  // gather + un-permute timing
     uint32_t W = 0, H = 0, rows_max = 0;
     uint64_t frames = 0;
     int last = -1;  // buffer set of the last frame
@@ -142,13 +146,13 @@ namespace {
 void free_buffers(MultiRender* m) {
     for (int d = 0; d < m->n; ++d) {
         Guard g(m->first + d);
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < PIPE; ++s) {
             if (m->dev[d].rows[s]) (void)hipFree(m->dev[d].rows[s]);
             m->dev[d].rows[s] = nullptr;
         }
     }
     Guard g(m->first);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < PIPE; ++s) {
         if (m->staging[s]) (void)hipFree(m->staging[s]);
         m->staging[s] = nullptr;
     }
@@ -160,7 +164,7 @@ void free_buffers(MultiRender* m) {
 void sync_all(MultiRender* m) {
     for (int d = 0; d < m->n; ++d) {
         Guard g(m->first + d);
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < PIPE; ++s)
             if (m->dev[d].rs[s]) (void)hipStreamSynchronize(m->dev[d].rs[s]);
         if (m->dev[d].cs) (void)hipStreamSynchronize(m->dev[d].cs);
     }
@@ -178,13 +182,13 @@ void ensure_buffers(MultiRender* m, uint32_t W, uint32_t H) {
     const size_t shard = (size_t)rows_max * W * 3 * sizeof(float);
     for (int d = 0; d < m->n; ++d) {
         Guard g(m->first + d);
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < PIPE; ++s) {
             hcheck(hipMalloc((void**)&m->dev[d].rows[s], shard), "hipMalloc(row shard)");
             hcheck(hipMemset(m->dev[d].rows[s], 0, shard), "hipMemset(row shard)");  // rows past a short shard
         }
     }
     Guard g(m->first);
-    for (int s = 0; s < 2; ++s) hcheck(hipMalloc((void**)&m->staging[s], shard * (size_t)m->n), "hipMalloc(staging)");
+    for (int s = 0; s < PIPE; ++s) hcheck(hipMalloc((void**)&m->staging[s], shard * (size_t)m->n), "hipMalloc(staging)");
     m->W = W;
     m->H = H;
     m->rows_max = rows_max;
@@ -210,7 +214,7 @@ MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes) {
         for (int d = 0; d < m->n; ++d) {
             Guard g(m->first + d);
             MultiRender::Dev& x = m->dev[(size_t)d];
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < PIPE; ++s) {
                 hcheck(hipStreamCreateWithFlags(&x.rs[s], hipStreamNonBlocking), "hipStreamCreate");
                 hcheck(hipEventCreateWithFlags(&x.rendered[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreateWithFlags(&x.gathered[s], hipEventDisableTiming), "hipEventCreate");
@@ -222,7 +226,7 @@ MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes) {
         {
             Guard g(m->first);
             hcheck(hipStreamCreateWithFlags(&m->host_stream, hipStreamNonBlocking), "hipStreamCreate");
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < PIPE; ++s) {
                 hcheck(hipEventCreateWithFlags(&m->in_ev[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreateWithFlags(&m->done_ev[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreate(&m->g0[s]), "hipEventCreate");
@@ -259,7 +263,7 @@ void gpu_multi_free(MultiRender* m) {
     for (int d = 0; d < m->n; ++d) {
         Guard g(m->first + d);
         MultiRender::Dev& x = m->dev[(size_t)d];
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < PIPE; ++s) {
             for (hipEvent_t e : {x.rendered[s], x.gathered[s], x.t0[s], x.t1[s]})
                 if (e) (void)hipEventDestroy(e);
             if (x.rs[s]) (void)hipStreamDestroy(x.rs[s]);
@@ -268,7 +272,7 @@ void gpu_multi_free(MultiRender* m) {
     }
     {
         Guard g(m->first);
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < PIPE; ++s)
             for (hipEvent_t e : {m->in_ev[s], m->done_ev[s], m->g0[s], m->g1[s]})
                 if (e) (void)hipEventDestroy(e);
         if (m->host_stream) (void)hipStreamDestroy(m->host_stream);
@@ -287,7 +291,7 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
              hipStream_t stream) {
     const Rccl& r = rccl();
     ensure_buffers(m, p0.width, p0.height);
-    const int s = (int)(m->frames & 1u);
+    const int s = (int)(m->frames % PIPE);
     const uint32_t N = (uint32_t)m->n;
     {
         Guard g(m->first);
@@ -296,7 +300,7 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
     for (int d = 0; d < m->n; ++d) {
         Guard g(m->first + d);
         MultiRender::Dev& x = m->dev[(size_t)d];
-        // rows[s] is free once the gather of frame k - 2 has read it
+        // rows[s] is free once the gather of frame k - PIPE has read it
         hcheck(hipStreamWaitEvent(x.rs[s], x.gathered[s], 0), "hipStreamWaitEvent");
         RenderParams q = p0;
         q.row_offset = (uint32_t)d;
@@ -379,7 +383,7 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
             hcheck(hipEventElapsedTime(&ms, m->g0[s], m->g1[s]), "hipEventElapsedTime");
         } else if (m->frames >= 2) {  // first device: the previous frame's render end -> this one's
             Guard g(m->first);
-            hcheck(hipEventElapsedTime(&ms, m->dev[0].t1[1 - s], m->dev[0].t1[s]), "hipEventElapsedTime");
+            hcheck(hipEventElapsedTime(&ms, m->dev[0].t1[(s + PIPE - 1) % PIPE], m->dev[0].t1[s]), "hipEventElapsedTime");
         }
         if ((size_t)d < n) out[d] = ms;
     }

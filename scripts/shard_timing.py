@@ -8,7 +8,7 @@ Each N is timed two ways: `shard_ms` brackets one launch with events after a syn
 launch work, occupancy queries and hipModuleLaunchKernel, counts when the GPU waits for it), and
 `shard_ms_queued` the same launch enqueued behind a previous one, so the GPU is still busy while the
 host prepares it (as in bench.py's double-buffered loop): the kernel alone.  `shard_ms_pipelined`:
-K launches alternating over SHARD_STREAMS (default 2) streams and buffers (the library's multi-GPU render does this,
+K launches alternating over SHARD_STREAMS (default 2, as bench.py and the library) streams and buffers (the library's multi-GPU render does this,
 csrc/multi.hip), total device time / K: launch k+1's workgroups take the SIMDs launch k's last paths
 leave idle, so the per-launch tail overlaps the next launch's start.
 """

@@ -132,7 +132,7 @@ def test_library_multi_gpu_device_api_pipelined():
     with in_golden():
         s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
     want = s.render(precision="f32", rng="philox", device=0)
-    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0") for _ in range(3)]
+    outs = [torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0") for _ in range(5)]  # > the 3 buffer sets
     st = torch.cuda.current_stream(0)
     for o in outs:
         s.render_device(o.data_ptr(), o.numel(), precision="f32", rng="philox", device=0, stream=st.cuda_stream, gpus=1)
