@@ -419,17 +419,17 @@ def run_library(args):
         scene.upload(d)
     t_upload = time.perf_counter() - t0
     stream = torch.cuda.current_stream()
-    D = max(1, args.pipeline)  # device / pinned host frames (the library keeps its own buffer sets)
-    frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(D)]
-    host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(D)]
+    NB = max(2, args.pipeline)  # device / pinned host frames (the library keeps its own buffer sets)
+    frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
+    host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(NB)]
     copy_stream = torch.cuda.Stream(device=dev)
-    copied = [None] * D
+    copied = [None] * NB
     cev = []
 
     def step(k, timed):
-        slot = k % D
+        slot = k % NB
         if copied[slot] is not None:
-            stream.wait_event(copied[slot])  # frame `slot` was copied out D frames ago
+            stream.wait_event(copied[slot])  # frame `slot` was copied out NB frames ago
         scene.render_device(frames[slot].data_ptr(), H * W * 3, precision=args.precision, rng=args.rng, device=0,
                             stream=stream.cuda_stream, trace=args.trace, gpus=N)
         if not args.kernel_only:
@@ -461,7 +461,7 @@ def run_library(args):
     tm = scene.render_timings()  # the last timed frame's per-device kernel and gather times
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
     jit_after = nrt.jit_stats()
-    last = host[(args.warmup + args.steps - 1) % D].numpy()
+    last = host[(args.warmup + args.steps - 1) % NB].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
     # GPU 0's render-to-render period (the frames' renders overlap at their ends, as with --pipeline > 1)
@@ -554,23 +554,24 @@ def run_ranks(args):
     # D = --pipeline row buffers rendered on D streams (D = 1: one stream); N = 1: the row buffers are
     # the frames; N > 1: rank 0 gathers into D frames.  Pinned host frames, one per buffer.
     D = max(1, args.pipeline)
-    rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(D)]
+    NB = max(2, D)  # buffers: at least two, so frame k's host copy overlaps frame k+1's render
+    rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
     rstreams = [torch.cuda.Stream(device=dev) for _ in range(D)] if D > 1 else [stream]
-    freed = [None] * D  # event: rbuf[slot] consumed (copied to the host, or gathered)
+    freed = [None] * NB  # event: rbuf[slot] consumed (copied to the host, or gathered)
     if lead:
         frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
-                                          for _ in range(D)]
-        host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(D)]
+                                          for _ in range(NB)]
+        host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(NB)]
         copy_stream = torch.cuda.Stream(device=dev)
-        copied = [None] * D
+        copied = [None] * NB
     rend, cev = [], []
     single = {}
 
     def step(k, timed, isolated=False):
-        slot = k % D
-        rs = rstreams[slot]
+        slot = k % NB
+        rs = rstreams[k % D]
         if freed[slot] is not None:
-            rs.wait_event(freed[slot])  # rbuf[slot] was consumed D frames ago
+            rs.wait_event(freed[slot])  # rbuf[slot] was consumed NB frames ago
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(rs)
         scene.render_device(rbuf[slot].data_ptr(), rows * W * 3, precision=args.precision, rng=args.rng,
@@ -585,7 +586,7 @@ def run_ranks(args):
             stream.wait_event(e1)
             fr = frames[slot] if lead else None
             if lead and copied[slot] is not None:
-                stream.wait_event(copied[slot])  # frame buffer `slot` was copied out D frames ago
+                stream.wait_event(copied[slot])  # frame buffer `slot` was copied out NB frames ago
             shard.gather_frame(rbuf[slot], H, dist, rank, world, out=fr, host=args.backend == "gloo")
             ready = torch.cuda.Event()
             ready.record(stream)
@@ -646,7 +647,7 @@ def run_ranks(args):
         mixed = float(t[2]) != -float(t[3])
     variant = kernel_variant_of(jit_before, jit_after, args.steps, mixed)
     if lead:
-        last = host[(args.warmup + args.steps - 1) % D].numpy()
+        last = host[(args.warmup + args.steps - 1) % NB].numpy()
         frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
         report(args, nrt, scene, n_gpus=world, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
                timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
