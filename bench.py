@@ -659,7 +659,8 @@ def run_ranks(args):
                                         None if single_ms is None else round(single_ms, 3),
                                         "note": "kernel_ms = device time between successive render completions "
                                                 "(the steady-state time per frame's render); single_frame_render_ms "
-                                                "= one render alone on the GPU (the last warm-up frame)"}},
+                                                "= one render alone on an idle GPU (the last warm-up frame, after a "
+                                                "synchronize: launch latency and clock ramp included)"}},
                           **({"multi_gpu": {"path": "ranks", "backend": args.backend}} if world > 1 else {})))
     if world > 1:
         dist.barrier()
