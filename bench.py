@@ -494,7 +494,19 @@ def main():
                           "cpu_baseline": cpu}), flush=True)
         return 0
 
-    launched = "WORLD_SIZE" in os.environ
+    path = choose_path(args, "WORLD_SIZE" in os.environ)
+    if path == "library":
+        return run_library(args)
+    if path == "launch":
+        # one process per GPU, no launcher: torch.distributed.run as a child (nothing has touched the GPU)
+        return launch_ranks_child(args)
+    return run_ranks(args)
+
+
+def choose_path(args, launched):
+    """Which N-GPU step this invocation runs: "library" (one process, nrt_render_opts.gpus), "launch"
+    (start torch.distributed.run as a child, one process per GPU), or "ranks" (this process is a rank,
+    or N = 1 on the single-device path)."""
     multi = args.multi
     if multi == "auto":
         multi = "ranks" if launched or (args.gpus > 1 and args.backend == "gloo") else (
@@ -502,11 +514,10 @@ def main():
     if multi == "library":
         if launched:
             raise SystemExit("--multi library runs in one process: start it without torch.distributed.run")
-        return run_library(args)
+        return "library"
     if not launched and args.gpus > 1:
-        # one process per GPU, no launcher: torch.distributed.run as a child (nothing has touched the GPU)
-        return launch_ranks_child(args)
-    return run_ranks(args)
+        return "launch"
+    return "ranks"
 
 
 def run_ranks(args):

@@ -72,6 +72,9 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_CAM_RELOAD
 #define NRT_CAM_RELOAD 0  // f32 camera vectors: scalar loads from the kernel arguments at the use
 #endif
+#ifndef NRT_CHACHA_TOPUP
+#define NRT_CHACHA_TOPUP 1  // ChaCha8 ring refilled at the persistent loop's head (ChaCha8::top_up)
+#endif
 constexpr int RING = 16;  // ChaCha8 ring: 2 blocks of 8 u64 draws per lane, in LDS
 // ChaCha8 (persistent-lane) kernels' dynamic LDS before the stack and the staged scene: the ring,
 // then each lane's f64 pixel sums (kept in LDS, not registers: the earth scene's exact kernel spilled
@@ -251,7 +254,19 @@ struct ChaCha8 {
         ensure(1);
         return take();
     }
+    // At a point the whole wave reaches (the persistent loop's head): every lane with room for a
+    // block generates one, together, so the samplers' own refills (inside divergent code: a
+    // rejection loop runs with only its still-trying lanes) become rare.  Refill timing never
+    // changes the words or their order.
+    __device__ __forceinline__ void top_up() {
+        if (count <= RING - 8) refill();
+    }
 };
+// Philox and other counter-based generators: nothing to top up
+template <class G>
+__device__ __forceinline__ void rng_top_up(G& g) {
+    if constexpr (G::uses_lds) g.top_up();
+}
 
 // Philox4x32-10 (Salmon et al. 2011), counter = (pixel, sample, pair, 0), key = (0, 0).
 // Rounds 1-9 mix the round key into one word with one v_bitop3_b32 (hi ^ c ^ key):
@@ -2991,6 +3006,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     if (going) wbvh_step<R, FLAT, SIG>(ts, gsc, ray, stack);
                 }
                 const unsigned long long t1 = stamp();
+                if constexpr (NRT_CHACHA_TOPUP) {
+                    if (active) rng_top_up(g);
+                }
                 if (active && !ts.busy()) {
                     HitMin<R, MAXD> hm;
                     hm.t = ts.t_best;
@@ -3031,6 +3049,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (__ballot(have) == 0ull) break;  // (no lane holds a pixel: the counters are exhausted)
                 if (!have) continue;
                 const unsigned long long t0 = stamp();
+                if constexpr (NRT_CHACHA_TOPUP) rng_top_up(g);
                 if (fresh) {
                     camera_ray();  // (s < spp: a sample is left)
                     fresh = false;

@@ -60,3 +60,21 @@ def test_bench_work_block():
     assert bench.texel_payload_bytes({"texels": 0, "texel_bytes": 0, "texel_formats": 0}) == 0
     c3 = bench.load_work("scenes/earth.toml", 1920, 1080)
     assert c3["name"] == "C3" and c3["per_sample"]["texel_fetches"] > 0.2
+
+
+def test_bench_chooses_the_n_gpu_path():
+    """bench.py --gpus N as a driver may invoke it: without a launcher and with RCCL the library's
+    multi-GPU render (one process); with --backend gloo, or under torch.distributed.run, one process
+    per GPU (started as a child when there is no launcher); N = 1 the single-device path."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    c = lambda argv, launched=False: bench.choose_path(bench.parse_args(argv), launched)  # noqa: E731
+    assert c([]) == "ranks"
+    assert c(["--gpus", "8"]) == "library"
+    assert c(["--gpus", "8"], launched=True) == "ranks"
+    assert c(["--gpus", "2", "--backend", "gloo"]) == "launch"
+    assert c(["--gpus", "2", "--multi", "ranks"]) == "launch"
+    assert c(["--gpus", "1", "--multi", "library"]) == "library"
+    with pytest.raises(SystemExit):
+        c(["--gpus", "2", "--multi", "library"], launched=True)
