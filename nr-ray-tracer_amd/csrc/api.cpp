@@ -63,6 +63,8 @@ int guarded(int fail_code, F&& f) {
         return set_error(NRT_E_LOAD, e.what());
     } catch (const std::bad_alloc&) {
         return set_error(NRT_E_DEVICE, "out of memory");
+    } catch (const std::invalid_argument& e) {  // a bad argument, whichever call found it
+        return set_error(NRT_E_INVALID, e.what());
     } catch (const std::exception& e) {
         std::string m = e.what();
         if (m.find("outside the accelerated path") != std::string::npos) return set_error(NRT_E_UNSUPPORTED, m);

@@ -196,3 +196,18 @@ def test_scene_specialised_kernel_compiles(targs):
     assert nrt.debug_jit_compile(targs) > 4096
     with pytest.raises(nrt.NrtError):
         nrt.debug_jit_compile("float, nrt::dev::NoSuchRng, 0")
+
+
+def test_render_argument_errors_are_invalid():
+    """Bad render arguments are NRT_E_INVALID (-1) whether or not a GPU is present (checked before any
+    device work): gpus >= 1 renders the whole frame, so a row subset with it is refused."""
+    b = nrt.Builder()
+    m = b.lambertian(b.solid((1, 1, 1)))
+    scene = b.finish(b.bvh([b.sphere((0, 0, 0), 1.0, m)]))
+    cam = nrt.CameraBuilder(width=4, height=4, samples_per_pixel=1).build()
+    with pytest.raises(nrt.NrtError) as ei:
+        scene.render(cam, gpus=1, row_offset=1, row_stride=2)
+    assert ei.value.code == -1 and "whole frame" in str(ei.value)
+    with pytest.raises(nrt.NrtError) as ei:
+        scene.render(cam, precision="f32", rng="philox", device=10 ** 6)
+    assert ei.value.code in (-1, -3)  # device ordinal out of range (-1), or no GPU at all (-3)
