@@ -464,7 +464,8 @@ def run_library(args):
     last = host[(args.warmup + args.steps - 1) % NB].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
-    # GPU 0's render-to-render period (the frames' renders overlap at their ends, as with --pipeline > 1)
+    # GPU 0's frame-to-frame period (frame completions on its comm stream, in order; the renders overlap at
+    # their ends, as with --pipeline > 1)
     kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
     report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
@@ -476,10 +477,10 @@ def run_library(args):
                        f"(libnrt.so nrt_render_opts.gpus)",
            extra={"multi_gpu": {"path": "library", "launch_ms_per_gpu": [round(x, 3) for x in tm["kernel_ms"]],
                                 "gather_unpermute_ms": round(tm["gather_ms"], 3),
-                                "render_period_ms_gpu0": round(tm["period_ms"], 3),
+                                "frame_period_ms_gpu0": round(tm["period_ms"], 3),
                                 "note": "HIP-event times of the last timed frame (nrt_render_timings): each "
                                         "device's launch begin..end (overlapping the previous frame's tail), the "
-                                        "gather + un-permute on GPU 0, GPU 0's render-to-render period"}})
+                                        "gather + un-permute on GPU 0, the frame-to-frame period of the completions on GPU 0"}})
 
 
 def main():
@@ -589,7 +590,7 @@ def run_ranks(args):
                             device=local, row_offset=rank, row_stride=world, stream=rs.cuda_stream, trace=args.trace)
         e1.record(rs)
         if timed:
-            rend.append(e1)
+            rend.append((e0, e1))
         if isolated:
             single["ev"] = (e0, e1)
         ready = e1
@@ -638,10 +639,12 @@ def run_ranks(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # the render's device time per frame: successive render completions (with --pipeline > 1 the renders
-    # overlap at their ends, so one launch's own begin..end would count the other's tail)
-    if len(rend) >= 2:
-        kern_ms = rend[0].elapsed_time(rend[-1]) / (len(rend) - 1)
+    # the render's device time per frame: from the first timed render's start to the last render end, over
+    # the frames (with --pipeline > 1 consecutive renders overlap at their ends, and a frame may even end
+    # before the one launched just ahead of it on the other stream, so neither one launch's own begin..end
+    # nor the gap between successive end events is the time a frame costs)
+    if rend:
+        kern_ms = max(rend[0][0].elapsed_time(e1) for _, e1 in rend) / len(rend)
     else:
         kern_ms = single_ms if single_ms is not None else elapsed / max(args.steps, 1) * 1e3
     d2h_ms = sum(a.elapsed_time(b) for a, b in cev) / max(len(cev), 1) if cev else 0.0
@@ -668,8 +671,8 @@ def run_ranks(args):
                parallelism=f"rows interleaved over {world} GPU(s), one RCCL gather to rank 0",
                extra=dict({"pipeline": {"frames_in_flight": D, "single_frame_render_ms":
                                         None if single_ms is None else round(single_ms, 3),
-                                        "note": "kernel_ms = device time between successive render completions "
-                                                "(the steady-state time per frame's render); single_frame_render_ms "
+                                        "note": "kernel_ms = device time from the first timed render's start to the "
+                                                "last render's end, per frame; single_frame_render_ms "
                                                 "= one render alone on an idle GPU (the last warm-up frame, after a "
                                                 "synchronize: launch latency and clock ramp included)"}},
                           **({"multi_gpu": {"path": "ranks", "backend": args.backend}} if world > 1 else {})))

@@ -381,9 +381,9 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
             Guard g(m->first);
             hcheck(hipEventSynchronize(m->g1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->g0[s], m->g1[s]), "hipEventElapsedTime");
-        } else if (m->frames >= 2) {  // first device: the previous frame's render end -> this one's
+        } else if (m->frames >= 2) {  // the previous frame's un-permute end -> this one's (one stream: in order)
             Guard g(m->first);
-            hcheck(hipEventElapsedTime(&ms, m->dev[0].t1[(s + PIPE - 1) % PIPE], m->dev[0].t1[s]), "hipEventElapsedTime");
+            hcheck(hipEventElapsedTime(&ms, m->g1[(s + PIPE - 1) % PIPE], m->g1[s]), "hipEventElapsedTime");
         }
         if ((size_t)d < n) out[d] = ms;
     }
