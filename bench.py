@@ -452,6 +452,8 @@ def run_library(args):
             torch.cuda.synchronize()
             first_frame = time.perf_counter() - t_first0
     torch.cuda.synchronize()
+    if args.warmup:
+        scene.render_timings()  # (opens the frame-period window: the timed frames' completions follow)
     jit_before = nrt.jit_stats()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -464,8 +466,8 @@ def run_library(args):
     last = host[(args.warmup + args.steps - 1) % NB].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
-    # GPU 0's frame-to-frame period (frame completions on its comm stream, in order; the renders overlap at
-    # their ends, as with --pipeline > 1)
+    # the mean time between the timed frames' completions on GPU 0's comm stream (frames in order; the renders
+    # overlap at their ends, as with --pipeline > 1): the device time a frame costs
     kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
     report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
@@ -480,7 +482,7 @@ def run_library(args):
                                 "frame_period_ms_gpu0": round(tm["period_ms"], 3),
                                 "note": "HIP-event times of the last timed frame (nrt_render_timings): each "
                                         "device's launch begin..end (overlapping the previous frame's tail), the "
-                                        "gather + un-permute on GPU 0, the frame-to-frame period of the completions on GPU 0"}})
+                                        "gather + un-permute on GPU 0, the mean frame-to-frame period of the timed frames' completions on GPU 0"}})
 
 
 def main():

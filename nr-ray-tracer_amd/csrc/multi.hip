@@ -135,6 +135,11 @@ struct MultiRender {
     hipStream_t host_stream = nullptr;
     hipEvent_t in_ev[PIPE] = {}, done_ev[PIPE] = {};
     hipEvent_t g0[PIPE] = {}, g1[PIPE] = {};  // gather + un-permute timing
+    // frame-period window (nrt_render_timings): w0 = the first frame's completion on the first device's
+    // comm stream since the last read, w_frames = frames completed after it
+    hipEvent_t w0 = nullptr;
+    bool w_armed = false;
+    uint64_t w_frames = 0;
     uint32_t W = 0, H = 0, rows_max = 0;
     uint64_t frames = 0;
     int last = -1;  // buffer set of the last frame
@@ -226,6 +231,7 @@ MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes) {
         {
             Guard g(m->first);
             hcheck(hipStreamCreateWithFlags(&m->host_stream, hipStreamNonBlocking), "hipStreamCreate");
+            hcheck(hipEventCreate(&m->w0), "hipEventCreate");
             for (int s = 0; s < PIPE; ++s) {
                 hcheck(hipEventCreateWithFlags(&m->in_ev[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreateWithFlags(&m->done_ev[s], hipEventDisableTiming), "hipEventCreate");
@@ -275,6 +281,7 @@ void gpu_multi_free(MultiRender* m) {
         for (int s = 0; s < PIPE; ++s)
             for (hipEvent_t e : {m->in_ev[s], m->done_ev[s], m->g0[s], m->g1[s]})
                 if (e) (void)hipEventDestroy(e);
+        if (m->w0) (void)hipEventDestroy(m->w0);
         if (m->host_stream) (void)hipStreamDestroy(m->host_stream);
     }
     delete m;
@@ -341,6 +348,13 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
                        m->rows_max, m->W * 3u);
     hcheck(hipGetLastError(), "un-permute launch");
     hcheck(hipEventRecord(m->g1[s], cs0), "hipEventRecord");
+    if (!m->w_armed) {
+        hcheck(hipEventRecord(m->w0, cs0), "hipEventRecord");
+        m->w_armed = true;
+        m->w_frames = 0;
+    } else {
+        ++m->w_frames;
+    }
     hcheck(hipEventRecord(m->done_ev[s], cs0), "hipEventRecord");
     hcheck(hipStreamWaitEvent(stream, m->done_ev[s], 0), "hipStreamWaitEvent");
     m->last = s;
@@ -381,12 +395,14 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
             Guard g(m->first);
             hcheck(hipEventSynchronize(m->g1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->g0[s], m->g1[s]), "hipEventElapsedTime");
-        } else if (m->frames >= 2) {  // the previous frame's un-permute end -> this one's (one stream: in order)
+        } else if (m->w_armed && m->w_frames > 0) {  // mean completion-to-completion time over the window
             Guard g(m->first);
-            hcheck(hipEventElapsedTime(&ms, m->g1[(s + PIPE - 1) % PIPE], m->g1[s]), "hipEventElapsedTime");
+            hcheck(hipEventElapsedTime(&ms, m->w0, m->g1[s]), "hipEventElapsedTime");
+            ms /= (float)m->w_frames;
         }
         if ((size_t)d < n) out[d] = ms;
     }
+    if (n > (size_t)m->n + 1) m->w_armed = false;  // read: the next frame opens a new window (a size query keeps it)
     return (size_t)m->n + 2;
 }
 

@@ -11,3 +11,8 @@ python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read())
 print('bench', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['pipeline'], d['cpu_baseline']['value'], d['timings_s'], d['frame_sha256'][:16])" gpurun_out/${tag}_bench.json
+timeout -k 10 300 python bench.py --no-cpu-baseline --multi library --gpus 1 > gpurun_out/${tag}_lib1.json 2> gpurun_out/${tag}_lib1.err || { tail -5 gpurun_out/${tag}_lib1.err; exit 1; }
+python3 -c "
+import json,sys
+d=json.loads(open(sys.argv[1]).read())
+print('lib1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['multi_gpu'], d['frame_sha256'][:16])" gpurun_out/${tag}_lib1.json
