@@ -466,8 +466,8 @@ def run_library(args):
     last = host[(args.warmup + args.steps - 1) % NB].numpy()
     frame_sha = None if args.kernel_only else hashlib.sha256(last.tobytes()).hexdigest()
     rows = scene.rows_selected(H, 0, N)
-    # the mean time between the timed frames' completions on GPU 0's comm stream (frames in order; the renders
-    # overlap at their ends, as with --pipeline > 1): the device time a frame costs
+    # the device time per timed frame: GPU 0's first timed render start to the last frame's completion, over
+    # the frames (the renders overlap at their ends, as with --pipeline > 1)
     kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
     report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
@@ -479,10 +479,10 @@ def run_library(args):
                        f"(libnrt.so nrt_render_opts.gpus)",
            extra={"multi_gpu": {"path": "library", "launch_ms_per_gpu": [round(x, 3) for x in tm["kernel_ms"]],
                                 "gather_unpermute_ms": round(tm["gather_ms"], 3),
-                                "frame_period_ms_gpu0": round(tm["period_ms"], 3),
+                                "frame_ms_gpu0": round(tm["period_ms"], 3),
                                 "note": "HIP-event times of the last timed frame (nrt_render_timings): each "
                                         "device's launch begin..end (overlapping the previous frame's tail), the "
-                                        "gather + un-permute on GPU 0, the mean frame-to-frame period of the timed frames' completions on GPU 0"}})
+                                        "gather + un-permute on GPU 0, the device time per timed frame on GPU 0 (first render start to last completion, over the frames)"}})
 
 
 def main():

@@ -261,9 +261,9 @@ int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nr
 /* HIP-event times (ms) of the scene's last gpus >= 1 render (waits for it): out[d] = the render
  * launch on device first+d, d < N (begin to end; consecutive frames overlap, so this can include the
  * previous frame's tail); out[N] = the gather + un-permute on the first device (from its own render's
- * end, so the slowest device's lag is in it); out[N+1] = the mean time between consecutive frame
- * completions (gather + un-permute done, one stream: frames in order) since the previous call of this
- * function that wrote it, the steady-state time per frame (0 with fewer than two frames); a call that
+ * end, so the slowest device's lag is in it); out[N+1] = the device time per frame since the previous
+ * call that wrote it: from the first device's render start of that window's first frame to the last
+ * frame's completion (gather + un-permute done), over the frames (0 with fewer than two); a call that
  * writes out[N+1] starts a new window.  *count = N + 2; at most n written. */
 int nrt_render_timings(const nrt_scene* scene, float* out, size_t n, size_t* count);
 /* Number of rows selected by opts for an image of `height` rows. */

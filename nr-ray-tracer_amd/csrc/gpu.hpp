@@ -28,9 +28,9 @@ void gpu_multi_render_device(MultiRender* m, const RenderParams& p, uint32_t pre
 void gpu_multi_render_host(MultiRender* m, const RenderParams& p, uint32_t precision, uint32_t rng, uint32_t trace,
                            float* host_out);
 // HIP-event times (ms) of the last frame: out[d] = device first + d's render kernel, out[N] = the
-// gather + un-permute on the first device, out[N + 1] = the mean time between consecutive frame
-// completions on the first device's comm stream since the previous call (frames in order; 0 with
-// fewer than two frames); a call that writes out[N + 1] starts a new window; returns N + 2
+// gather + un-permute on the first device, out[N + 1] = the device time per frame since the previous
+// call: the first device's render start of the window's first frame to the last frame's completion,
+// over the frames (0 with fewer than two); a call that writes out[N + 1] starts a new window; returns N + 2
 size_t gpu_multi_timings(MultiRender* m, float* out, size_t n);
 
 int gpu_device_count();

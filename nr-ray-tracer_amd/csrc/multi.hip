@@ -135,8 +135,9 @@ struct MultiRender {
     hipStream_t host_stream = nullptr;
     hipEvent_t in_ev[PIPE] = {}, done_ev[PIPE] = {};
     hipEvent_t g0[PIPE] = {}, g1[PIPE] = {};  // gather + un-permute timing
-    // frame-period window (nrt_render_timings): w0 = the first frame's completion on the first device's
-    // comm stream since the last read, w_frames = frames completed after it
+    // frame-period window (nrt_render_timings): w0 = the start of the first device's render of the
+    // window's first frame, w_frames = frames enqueued in the window (consecutive frames' renders overlap,
+    // so a window from a completion would miss the first frame's share and over-count the others)
     hipEvent_t w0 = nullptr;
     bool w_armed = false;
     uint64_t w_frames = 0;
@@ -317,6 +318,14 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
         q.pixel_end = q.rows * q.width;
         q.out = x.rows[s];
         hcheck(hipEventRecord(x.t0[s], x.rs[s]), "hipEventRecord");
+        if (d == 0) {
+            if (!m->w_armed) {
+                hcheck(hipEventRecord(m->w0, x.rs[s]), "hipEventRecord");
+                m->w_armed = true;
+                m->w_frames = 0;
+            }
+            ++m->w_frames;
+        }
         gpu_launch_render(m->scenes[(size_t)d], q, precision, rng, trace, x.rs[s]);
         hcheck(hipEventRecord(x.t1[s], x.rs[s]), "hipEventRecord");
         hcheck(hipEventRecord(x.rendered[s], x.rs[s]), "hipEventRecord");
@@ -348,13 +357,6 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
                        m->rows_max, m->W * 3u);
     hcheck(hipGetLastError(), "un-permute launch");
     hcheck(hipEventRecord(m->g1[s], cs0), "hipEventRecord");
-    if (!m->w_armed) {
-        hcheck(hipEventRecord(m->w0, cs0), "hipEventRecord");
-        m->w_armed = true;
-        m->w_frames = 0;
-    } else {
-        ++m->w_frames;
-    }
     hcheck(hipEventRecord(m->done_ev[s], cs0), "hipEventRecord");
     hcheck(hipStreamWaitEvent(stream, m->done_ev[s], 0), "hipStreamWaitEvent");
     m->last = s;
@@ -395,7 +397,7 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
             Guard g(m->first);
             hcheck(hipEventSynchronize(m->g1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->g0[s], m->g1[s]), "hipEventElapsedTime");
-        } else if (m->w_armed && m->w_frames > 0) {  // mean completion-to-completion time over the window
+        } else if (m->w_armed && m->w_frames > 1) {  // window start -> last completion, per frame
             Guard g(m->first);
             hcheck(hipEventElapsedTime(&ms, m->w0, m->g1[s]), "hipEventElapsedTime");
             ms /= (float)m->w_frames;

@@ -8,5 +8,5 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --multi library --gpus 1 > g
 python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read())
-print('lib1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['multi_gpu']['frame_period_ms_gpu0'], d['frame_sha256'][:16])" gpurun_out/${tag}_lib1.json
+print('lib1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['multi_gpu']['frame_ms_gpu0'], d['frame_sha256'][:16])" gpurun_out/${tag}_lib1.json
 done
