@@ -6,8 +6,8 @@ With bench.py --pipeline 1 consecutive frames' render launches overlap at their 
 workgroups start on the SIMDs frame k's last paths leave idle), so one dispatch's begin..end also
 counts the other frame's tail and rocprofv3's AverageNs exceeds the time a frame costs.  This prints,
 per render-kernel name: dispatches, the mean begin..end duration (what --stats averages), the
-steady-state period = (last end - first end) / (n - 1) over the dispatches after the first two
-(warm-up / module load), which is what bench.py's roofline.kernel_ms measures with HIP events, and
+steady-state period = (last end - first start) / n over the dispatches after the first two (warm-up /
+module load), which is what bench.py's roofline.kernel_ms measures with HIP events, and
 the overlap between consecutive dispatches.
 """
 import argparse
@@ -41,7 +41,10 @@ def main():
         d.sort(key=lambda x: x[1])
         dur = [e - s for s, e in d]
         steady = d[a.skip:] if len(d) > a.skip + 1 else d
-        period = (steady[-1][1] - steady[0][1]) / (len(steady) - 1) if len(steady) > 1 else None
+        # first start to last end over the steady dispatches, per dispatch (consecutive dispatches
+        # overlap, and one may even end before the one launched just ahead of it: end-to-end gaps
+        # alone are biased)
+        period = (max(e for _, e in steady) - min(s for s, _ in steady)) / len(steady)
         overlap = [max(0, d[i][1] - d[i + 1][0]) for i in range(len(d) - 1)]
         out[name] = {"dispatches": len(d), "mean_duration_ns": sum(dur) / len(dur),
                      "steady_period_ns": period, "steady_dispatches": len(steady),
