@@ -181,7 +181,7 @@ struct alignas(16) DBvhNode {
 // measured 20 % slower on the teapot (C4 40.3 -> 48.5 ms, round 3).
 struct alignas(16) DBvh4Node {
     float org[3];      // lower corner of the node's box
-    uint32_t exps;     // scale exponent byte per axis (bits 0-7 x, 8-15 y, 16-23 z)
+    uint32_t exps;     // quantization step per axis, 10 bits each (x bits 0-9, y 10-19, z 20-29): wbvh_step
     uint32_t qlo[3];   // per axis, byte k = child k's low plane
     uint32_t qhi[3];   // per axis, byte k = child k's high plane
     int32_t child[4];  // refs as in DBvhNode (inner = DBvh4Node index), WBVH_DONE = empty slot
@@ -316,6 +316,12 @@ NRT_HD inline uint64_t tex_rgb8_byte(uint32_t x, uint32_t y, uint32_t tiles_per_
     const uint32_t ty = (y * 52429u) >> 18, ly = y - 5u * ty;
     return ((uint64_t)ty * tiles_per_row + (x >> 3)) * 128u + (ly * 8u + (x & 7u)) * 3u;
 }
+// World BVH 4-wide nodes: the quantization step of axis a, 2^e (1 + m / 4) from its 10-bit field
+// (e + 127) << 2 | m: the field shifted into an f32's exponent and top two mantissa bits, exactly
+#ifndef NRT_WBVH_STEP_MANTISSA
+#define NRT_WBVH_STEP_MANTISSA 1  // 0: powers of two only (the round-4 steps)
+#endif
+NRT_HD inline uint32_t wbvh_step_bits(uint32_t exps, int a) { return ((exps >> (10 * a)) & 0x3FFu) << 21; }
 // PAL16: 16-bit word index of texel (x, y) in the index array (two texels per 32-bit word), and
 // the words the index array takes
 NRT_HD inline uint64_t tex_pal_index(uint32_t x, uint32_t y, uint32_t tiles_per_row) {

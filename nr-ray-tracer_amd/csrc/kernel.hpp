@@ -1263,9 +1263,9 @@ template <typename R, class STK>
 __device__ __forceinline__ void wbvh4_visit(WbvhTrav& t, const DSceneView<R>& sc, STK& stack) {
     const DBvh4Node nd = load16(sc.wbvh4 + t.node);
     // plane t = (org + q * step - o) / d = q * (step / d) + (org / d - o / d)
-    const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
-    const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
-    const float Az = __uint_as_float(((nd.exps >> 16) & 0xFFu) << 23) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
+    const float Ax = __uint_as_float(wbvh_step_bits(nd.exps, 0)) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
+    const float Ay = __uint_as_float(wbvh_step_bits(nd.exps, 1)) * t.iy, By = nd.org[1] * t.iy - t.oy;
+    const float Az = __uint_as_float(wbvh_step_bits(nd.exps, 2)) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
     // The ray's direction signs pick each axis's near and far plane bytes for all four
     // children at once (1/d is finite, wbvh_begin), so a child's slab needs no min/max, and an
     // empty slot (qlo 255, qhi 0 on every axis) comes out with near > far: a miss.
@@ -1333,9 +1333,9 @@ __device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& s
 }
 template <class STK>
 __device__ __forceinline__ void wbvh4c_visit_nd(WbvhTrav& t, const DBvh4cNode& nd, STK& stack) {
-    const float Ax = __uint_as_float((nd.exps & 0xFFu) << 23) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
-    const float Ay = __uint_as_float(((nd.exps >> 8) & 0xFFu) << 23) * t.iy, By = nd.org[1] * t.iy - t.oy;
-    const float Az = __uint_as_float(((nd.exps >> 16) & 0xFFu) << 23) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
+    const float Ax = __uint_as_float(wbvh_step_bits(nd.exps, 0)) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
+    const float Ay = __uint_as_float(wbvh_step_bits(nd.exps, 1)) * t.iy, By = nd.org[1] * t.iy - t.oy;
+    const float Az = __uint_as_float(wbvh_step_bits(nd.exps, 2)) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
     const bool px = t.ix >= 0.0f, py = t.iy >= 0.0f, pz = t.iz >= 0.0f;
     const uint32_t nqx = px ? nd.qlo[0] : nd.qhi[0], fqx = px ? nd.qhi[0] : nd.qlo[0];
     const uint32_t nqy = py ? nd.qlo[1] : nd.qhi[1], fqy = py ? nd.qhi[1] : nd.qlo[1];
