@@ -247,7 +247,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
                          "prints one JSON line, no GPU is touched")
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=3,
                     help="frames whose renders may be in flight at once: consecutive renders rotate over this many "
                          "HIP streams and row buffers, so frame k+1's workgroups take the SIMDs frame k's last paths "
                          "leave idle (each frame is still one full render; ms_per_step = elapsed / steps); 1 (or 0): "
@@ -570,7 +570,10 @@ def run_ranks(args):
     D = max(1, args.pipeline)
     NB = max(2, D)  # buffers: at least two, so frame k's host copy overlaps frame k+1's render
     rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
-    rstreams = [torch.cuda.Stream(device=dev) for _ in range(D)] if D > 1 else [stream]
+    # (N = 1: the current stream is one of them, so D = 3 render streams and the copy stream stay within
+    # the process's 4 hardware queues; N > 1: it carries the gathers)
+    rstreams = ([stream] if world == 1 or D == 1 else []) + [torch.cuda.Stream(device=dev)
+                                                             for _ in range(D - (1 if world == 1 or D == 1 else 0))]
     freed = [None] * NB  # event: rbuf[slot] consumed (copied to the host, or gathered)
     if lead:
         frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
