@@ -247,11 +247,12 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the CPU baseline (the oracle on the host cores) for this config, e.g. BASELINE C1; "
                          "prints one JSON line, no GPU is touched")
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=None,
                     help="frames whose renders may be in flight at once: consecutive renders rotate over this many "
                          "HIP streams and row buffers, so frame k+1's workgroups take the SIMDs frame k's last paths "
                          "leave idle (each frame is still one full render; ms_per_step = elapsed / steps); 1 (or 0): "
-                         "each render waits for the previous one")
+                         "each render waits for the previous one.  Default 3 on one GPU, 2 with N > 1 (the gathers' "
+                         "streams share the process's 4 hardware queues)")
     ap.add_argument("--kernel-only", action="store_true",
                     help="diagnostics (PMC passes): no device-to-host copy of the frame, so device-wide counters "
                          "sampled over a render dispatch see the render kernel alone")
@@ -419,7 +420,7 @@ def run_library(args):
         scene.upload(d)
     t_upload = time.perf_counter() - t0
     stream = torch.cuda.current_stream()
-    NB = max(2, args.pipeline)  # device / pinned host frames (the library keeps its own buffer sets)
+    NB = max(2, args.pipeline or 2)  # device / pinned host frames (the library keeps its own buffer sets)
     frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
     host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(NB)]
     copy_stream = torch.cuda.Stream(device=dev)
@@ -567,7 +568,7 @@ def run_ranks(args):
     lead = rank == 0
     # D = --pipeline row buffers rendered on D streams (D = 1: one stream); N = 1: the row buffers are
     # the frames; N > 1: rank 0 gathers into D frames.  Pinned host frames, one per buffer.
-    D = max(1, args.pipeline)
+    D = max(1, args.pipeline if args.pipeline is not None else (3 if world == 1 else 2))
     NB = max(2, D)  # buffers: at least two, so frame k's host copy overlaps frame k+1's render
     rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
     # (N = 1: the current stream is one of them, so D = 3 render streams and the copy stream stay within
