@@ -323,7 +323,9 @@ def report(args, nrt, scene, *, n_gpus, rows, elapsed, kern_ms, d2h_ms, timings_
     tex_bytes = fetches * texel_b * rows * W * spp
     alg_bytes = fb_bytes + tex_bytes
     hbm_achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-    prof_s = pmc.get("avg_ns", 0) / 1e9 if pmc else 0
+    # the profiled kernel's time per launch: the steady period of the trace (scripts/trace_period.py; with frames
+    # in flight a dispatch's begin..end also spans its wait behind the ones ahead), else the stats' average
+    prof_s = (pmc.get("steady_period_ns") or pmc.get("avg_ns", 0)) / 1e9 if pmc else 0
     counter_gbs = traffic / prof_s / 1e9 if traffic and prof_s else None
     peak = VALU_PEAK_TFLOPS[args.precision]
     if wc is not None:
@@ -365,7 +367,7 @@ def report(args, nrt, scene, *, n_gpus, rows, elapsed, kern_ms, d2h_ms, timings_
                     "counter_gbs": None if counter_gbs is None else round(counter_gbs, 3),
                     "counter_frac": None if counter_gbs is None else counter_gbs / HBM_PEAK_GBS,
                     "traffic_over_algorithmic": None if not traffic else round(traffic / alg_bytes, 3)},
-            "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "valu_issue_frac", "valu_lane_utilization",
+            "pmc": {k: pmc.get(k) for k in ("kernel", "avg_ns", "steady_period_ns", "valu_issue_frac", "valu_lane_utilization",
                                             "valu_busy_est", "wait_inst_frac", "wait_any_frac", "hbm_fetch_bytes",
                                             "hbm_write_bytes", "tcc_hit_rate", "source")} if pmc else None,
             "note": "no dense contraction (no MFMA): the render kernel is bound by VALU issue and lane "

@@ -22,9 +22,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("--json")
-    ap.add_argument("--skip", type=int, default=2, help="leading dispatches left out of the period (warm-up)")
+    ap.add_argument("--skip", type=int, default=None,
+                    help="leading dispatches left out of the period (the warm-up frames; default: the `warmup` of the "
+                         "bench line next to the trace, bench_trace.json, else 2)")
     a = ap.parse_args()
     path = a.src
+    if a.skip is None:
+        a.skip = 2
+        bt = os.path.join(os.path.dirname(os.path.normpath(path if os.path.isdir(path) else os.path.dirname(path))),
+                          "bench_trace.json")
+        if os.path.exists(bt):
+            try:
+                a.skip = int(json.loads(open(bt).read().strip().splitlines()[-1])["warmup"])
+            except (ValueError, KeyError, IndexError):
+                pass
     if os.path.isdir(path):
         path = next(iter(glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)), None)
         if path is None:
@@ -40,11 +51,12 @@ def main():
     for name, d in rows.items():
         d.sort(key=lambda x: x[1])
         dur = [e - s for s, e in d]
-        steady = d[a.skip:] if len(d) > a.skip + 1 else d
+        steady = d[a.skip:]
         # first start to last end over the steady dispatches, per dispatch (consecutive dispatches
         # overlap, and one may even end before the one launched just ahead of it: end-to-end gaps
-        # alone are biased)
-        period = (max(e for _, e in steady) - min(s for s, _ in steady)) / len(steady)
+        # alone are biased); None with fewer than two (a run of 1-2 timed frames: the warm-up's host
+        # synchronize would sit inside the span)
+        period = ((max(e for _, e in steady) - min(s for s, _ in steady)) / len(steady)) if len(steady) >= 2 else None
         overlap = [max(0, d[i][1] - d[i + 1][0]) for i in range(len(d) - 1)]
         out[name] = {"dispatches": len(d), "mean_duration_ns": sum(dur) / len(dur),
                      "steady_period_ns": period, "steady_dispatches": len(steady),
