@@ -351,6 +351,11 @@ def report(args, nrt, scene, *, n_gpus, rows, elapsed, kern_ms, d2h_ms, timings_
             "unit": "TFLOP/s", "frac": None if achieved is None else round(achieved / peak, 4),
             "traffic": traffic,
             "flops_per_launch": flops_launch, "kernel_ms": round(kern_ms, 3),
+            "kernel_ms_basis": "device time per frame: the first timed render's start to the last render's end, over "
+                               "the frames (HIP events); frames in flight overlap, so a dispatch's own begin..end "
+                               "(rocprofv3 --stats AverageNs) also spans its wait behind the frames ahead: compare "
+                               "with scripts/trace_period.py's steady period of the same trace "
+                               "(profiles/*_trace_period.json, pmc.steady_period_ns)",
             "flops_source": None if wc is None else
             f"tests/golden/work_counts.json[{wc['name']}]: {wc['flops_per_sample']} algorithmic FLOPs/sample "
             f"(oracle event counts x SURVEY §8(d) per-event costs) x {rows * W * spp} samples per launch",
