@@ -587,7 +587,10 @@ def run_ranks(args):
         frames = rbuf if world == 1 else [torch.empty((H, W, 3), dtype=torch.float32, device=dev)
                                           for _ in range(NB)]
         host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(NB)]
-        copy_stream = torch.cuda.Stream(device=dev)
+        # D >= 4 on one GPU: each frame's host copy follows its render on the render's own stream (no copy
+        # stream: D render streams are all the hardware queues the process has)
+        copy_on_render = world == 1 and D >= 4
+        copy_stream = None if copy_on_render else torch.cuda.Stream(device=dev)
         copied = [None] * NB
     rend, cev = [], []
     single = {}
@@ -619,13 +622,15 @@ def run_ranks(args):
         else:
             freed[slot] = e1
         if lead and not args.kernel_only:
-            copy_stream.wait_event(ready)
+            cs = rs if copy_on_render else copy_stream
+            if not copy_on_render:
+                cs.wait_event(ready)
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             src = frames[slot]
-            with torch.cuda.stream(copy_stream):
-                c0.record(copy_stream)
+            with torch.cuda.stream(cs):
+                c0.record(cs)
                 host[slot].view(-1).copy_(src.view(-1)[: H * W * 3], non_blocking=True)
-                c1.record(copy_stream)
+                c1.record(cs)
             copied[slot] = c1
             if world == 1:
                 freed[slot] = c1
