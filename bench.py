@@ -433,6 +433,9 @@ def run_library(args):
     copy_stream = torch.cuda.Stream(device=dev)
     copied = [None] * NB
     cev = []
+    with torch.cuda.stream(copy_stream):  # (its hardware queue is created at its first launch)
+        torch.zeros(1, device=dev)
+    torch.cuda.synchronize()
 
     def step(k, timed):
         slot = k % NB
@@ -592,6 +595,12 @@ def run_ranks(args):
         copy_on_render = world == 1 and D >= 4
         copy_stream = None if copy_on_render else torch.cuda.Stream(device=dev)
         copied = [None] * NB
+    # HIP creates a stream's hardware queue at its first launch (milliseconds): touch every stream before
+    # the timed region even when there are fewer warm-up frames than streams
+    for st in rstreams + ([copy_stream] if lead and copy_stream is not None else []):
+        with torch.cuda.stream(st):
+            torch.zeros(1, device=dev)
+    torch.cuda.synchronize()
     rend, cev = [], []
     single = {}
 
