@@ -72,6 +72,15 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_CAM_RELOAD
 #define NRT_CAM_RELOAD 0  // f32 camera vectors: scalar loads from the kernel arguments at the use
 #endif
+#ifndef NRT_CHACHA_FAKE
+#define NRT_CHACHA_FAKE 0  // attribution builds: ChaCha8 blocks replaced by a cheap hash (frames differ)
+#endif
+#ifndef NRT_RIUS_WAVE
+#define NRT_RIUS_WAVE 1  // ChaCha8 rejection samplers as wave-converged loops (rejection_wave; see render_kernel)
+#endif
+#ifndef NRT_WALK_CONTRACT
+#define NRT_WALK_CONTRACT 1  // FMA contraction in the exact kernel's f32 culling walk and prefilter
+#endif
 #ifndef NRT_CHACHA_TOPUP
 #define NRT_CHACHA_TOPUP 1  // ChaCha8 ring refilled at the persistent loop's head (ChaCha8::top_up)
 #endif
@@ -227,7 +236,12 @@ struct ChaCha8 {
     __device__ __forceinline__ void start_sample(uint32_t) {}
     __device__ __forceinline__ void refill() {
         uint32_t w[16];
+#if NRT_CHACHA_FAKE  // attribution builds only (not the reference stream): a cheap stand-in for the block
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = (ctr * 16u + (uint32_t)k) * 0x9E3779B9u ^ s_lo;
+#else
         chacha8_block(ctr, 0u, s_lo, s_hi, w);
+#endif
         ++ctr;
         uint32_t slot = (head + count) & (RING - 1);
 #pragma unroll
@@ -451,6 +465,7 @@ __device__ __forceinline__ R draw_taken(G& g, R low, R high) {
 
 // vector.rs:61-70 — rejection in [-1,1)^3 until 1e-160 < |p|^2 <= 1, returns p/|p|^2
 template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sphere(G& g) {
+    const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
     while (true) {
         g.ensure(3);
         const R x = draw_taken<R>(g, R(-1), R(1));
@@ -458,7 +473,6 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_sp
         const R z = draw_taken<R>(g, R(-1), R(1));
         const V<R> p = mk(x, y, z);
         const R ls = dot(p, p);
-        const R tiny = sizeof(R) == 8 ? R(1e-160) : R(0);
         if (tiny < ls && ls <= R(1)) return vdiv(p, ls);
     }
 }
@@ -472,6 +486,34 @@ template <typename R, class G> __device__ __forceinline__ V<R> random_in_unit_di
         const R ls = dot(p, p);
         if (ls < R(1)) return vdiv(p, ls);
     }
+}
+
+// The two rejection samplers for the lanes with `need` set, called where the wave is converged:
+// when a needing lane is short of words, every lane with room refills (not only the lanes still
+// rejecting, as inside the samplers above), so the refills the wave executes serve most of its
+// lanes.  Same draws, same order, same result per lane; the other lanes get a zero vector.
+template <typename R, int D, class G>
+__device__ __forceinline__ V<R> rejection_wave(G& g, bool need) {
+    static_assert(G::uses_lds, "ChaCha8 streams only");
+    V<R> out = mk(R(0), R(0), R(0));
+    while (__ballot(need) != 0ull) {
+        if (__ballot(need && g.count < (uint32_t)D) != 0ull) {
+            if (g.count <= RING - 8) g.refill();
+        }
+        if (need) {
+            const R x = draw_taken<R>(g, R(-1), R(1));
+            const R y = draw_taken<R>(g, R(-1), R(1));
+            const R z = D == 3 ? draw_taken<R>(g, R(-1), R(1)) : R(0);
+            const V<R> q = mk(x, y, z);
+            const R ls = dot(q, q);
+            const bool ok = D == 3 ? ((sizeof(R) == 8 ? R(1e-160) : R(0)) < ls && ls <= R(1)) : ls < R(1);
+            if (ok) {
+                out = vdiv(q, ls);
+                need = false;
+            }
+        }
+    }
+    return out;
 }
 
 // Philox mode: the same distributions as the two rejection samplers, drawn
@@ -1333,6 +1375,12 @@ __device__ __forceinline__ void wbvh4c_visit(WbvhTrav& t, const DSceneView<R>& s
 }
 template <class STK>
 __device__ __forceinline__ void wbvh4c_visit_nd(WbvhTrav& t, const DBvh4cNode& nd, STK& stack) {
+#if NRT_WALK_CONTRACT
+    // FMAs in the exact kernel's culling walk too (its TU compiles without contraction): the walk
+    // only culls, and the boxes' outward rounding and padding cover one rounding as well as two
+    // (C4 f64 178 -> 169 ms, C5 f64 196 -> 191 ms, frames identical)
+#pragma clang fp contract(on)
+#endif
     const float Ax = __uint_as_float(wbvh_step_bits(nd.exps, 0)) * t.ix, Bx = nd.org[0] * t.ix - t.ox;
     const float Ay = __uint_as_float(wbvh_step_bits(nd.exps, 1)) * t.iy, By = nd.org[1] * t.iy - t.oy;
     const float Az = __uint_as_float(wbvh_step_bits(nd.exps, 2)) * t.iz, Bz = nd.org[2] * t.iz - t.oz;
@@ -1806,6 +1854,10 @@ __device__ __forceinline__ float absdot(V<float> a, V<float> b) {
 // when the reference test surely accepts the primitive
 __device__ __forceinline__ bool exact_prefilter(const DPrimWorld<float>& q, const Ray<float>& r, float& tlo,
                                                 float& thi, bool& certain) {
+#if NRT_WALK_CONTRACT
+    // (FMAs: one rounding where the bound E allows for two)
+#pragma clang fp contract(on)
+#endif
     constexpr float E = 0x1p-17f;
     const V<float> N = ld3(q.N);
     const float den = dot(N, r.d), aden = fabsf(den), eden = E * absdot(N, r.d);
@@ -2651,6 +2703,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     constexpr bool PERLIN = (KFLAGS & KF_PERLIN) != 0;
     constexpr bool FLAT = (KFLAGS & KF_FLAT) != 0;
     static_assert(!FLAT || (MAXD <= 0 && !PERLIN), "KF_FLAT is a world-list / world-BVH variant");
+    // ChaCha8 persistent-lane loop (MAXD >= 0): the rejection samplers run where the wave is converged
+    // and refill every lane with room (rejection_wave) instead of the loop head's top-up, for the
+    // plane-only exact variants and the f32 kernels: C5 f64 191.3 -> 187.5 ms, C5 f32 65.8 -> 63.6 ms;
+    // the textured earth's every-slot variant measured +4 % with them and keeps the top-up
+    constexpr bool RWAVE = NRT_RIUS_WAVE && G::uses_lds && MAXD >= 0 && ((KFLAGS & KF_PLANES) != 0 || sizeof(R) == 4);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // PROF slots: 0 iterations, 1 camera, 2 trace, 3 shade (= 5 + 6 + 7), 5 record + material,
     // 6 Philox block (+ sample claim), 7 scatter / camera ray + accumulate
@@ -2757,7 +2814,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     // Material::scatter (lambertian.rs:39-55, metal.rs:73-91, dielectric.rs:39-67)
     // into the next `ray`; false when a metal absorbs the ray (emitted = 0).  The
     // material is read again here rather than kept live across the RNG block.
-    auto scatter_ray = [&](const Rec<R>& h) -> bool {
+    // rs_pre: the unit-sphere draw already made by rejection_wave (RWAVE)
+    auto scatter_ray = [&](const Rec<R>& h, bool have_rs = false, V<R> rs_pre = V<R>{}) -> bool {
         const MatV<R> m = material(h.mat);
         V<R> dir;
         V<R> att = mk(R(1), R(1), R(1));
@@ -2777,7 +2835,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             dir = refl ? reflect(unit, h.n) : refract(unit, h.n, ri);
         } else {
             V<R> rs;
-            if constexpr (G::exact_stream) rs = random_in_unit_sphere<R>(g);
+            if constexpr (G::exact_stream) rs = have_rs ? rs_pre : random_in_unit_sphere<R>(g);
             else rs = unit_ball_inverse<R>(w.x, w.y, w.z);
             if (m.kind == MAT_LAMBERTIAN) {
                 dir = h.n + rs;
@@ -2936,8 +2994,8 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         if (have) start_pixel();
 
         // Camera::get_ray (camera.rs:244-267) of the pixel's next sample; false when all are done.
-        auto camera_ray = [&]() -> bool {
-            if (s >= p.spp) return false;
+        // (split in two around the disk draw for camera_ray_wave)
+        auto camera_point = [&]() -> V<R> {
             g.start_sample(s);
             ++s;
             R ox = R(0), oy = R(0);
@@ -2946,8 +3004,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 ox = draw_taken<R>(g, R(-0.5), R(0.5));
                 oy = draw_taken<R>(g, R(-0.5), R(0.5));
             }
-            const V<R> point = vfma((R)y + oy, cam(2), vfma((R)x + ox, cam(1), cam(0)));
-            const V<R> disk = random_in_unit_disk<R>(g);
+            return vfma((R)y + oy, cam(2), vfma((R)x + ox, cam(1), cam(0)));
+        };
+        auto camera_finish = [&](V<R> point, V<R> disk) {
             ray.o = vfma(disk.y, cam(5), vfma(disk.x, cam(4), cam(3)));
             ray.d = point - ray.o;
             ray.time = draw<R>(g, R(0.0), R(1.0));
@@ -2955,6 +3014,20 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             tp = mk(R(1), R(1), R(1));
             b = 0;
             bounced = false;  // Ray::bounce flag (Q4): 0 for camera rays
+        };
+        // the camera rays of the lanes with `go` set, the disk drawn where the wave is converged
+        // (RWAVE: rejection_wave)
+        auto camera_ray_wave = [&](bool go) {
+            V<R> point = mk(R(0), R(0), R(0));
+            if (go) point = camera_point();
+            const V<R> disk = rejection_wave<R, 2>(g, go);
+            if (go) camera_finish(point, disk);
+        };
+        auto camera_ray = [&]() -> bool {
+            if (s >= p.spp) return false;
+            const V<R> point = camera_point();
+            const V<R> disk = random_in_unit_disk<R>(g);
+            camera_finish(point, disk);
             return true;
         };
         // One shading step; true when the path continues with a new `ray`, otherwise
@@ -2966,7 +3039,15 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             V<R> contrib;
             const bool scatter = surface(traced, hit, hm, h, m, contrib);
             const unsigned long long s1 = stamp();
-            const bool cont = scatter && scatter_ray(h);
+            bool cont;
+            if constexpr (RWAVE) {
+                // lambertian and metal draw the unit-sphere vector first thing in scatter
+                // (dielectrics draw no vector): drawn here, where the wave is converged
+                const V<R> rs = rejection_wave<R, 3>(g, scatter && m.kind != MAT_DIELECTRIC);
+                cont = scatter && scatter_ray(h, m.kind != MAT_DIELECTRIC, rs);
+            } else {
+                cont = scatter && scatter_ray(h);
+            }
             if (!cont) {  // metal absorption adds contrib = 0
                 pacc[0] += (double)contrib.x;  // (the reference's f64 sum, in sample order)
                 pacc[BLOCK] += (double)contrib.y;
@@ -3049,8 +3130,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (__ballot(have) == 0ull) break;  // (no lane holds a pixel: the counters are exhausted)
                 if (!have) continue;
                 const unsigned long long t0 = stamp();
-                if constexpr (NRT_CHACHA_TOPUP) rng_top_up(g);
-                if (fresh) {
+                if constexpr (NRT_CHACHA_TOPUP && !RWAVE) rng_top_up(g);
+                if constexpr (RWAVE) {
+                    camera_ray_wave(fresh);  // (s < spp: a sample is left)
+                    fresh = false;
+                } else if (fresh) {
                     camera_ray();  // (s < spp: a sample is left)
                     fresh = false;
                 }

@@ -144,7 +144,10 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
             else launch_variant<R, G, MAXD, EXACT, false, 0, XS>(p, vw, ring, stream);
             return;
         }
-        if (planes && !perlin && !p.counters) {  // KF_PLANES: the 4-wave f64 variant
+#ifndef NRT_EXACT_PROF
+#define NRT_EXACT_PROF 0  // diagnostic builds: the phase profile (p.counters) of the LDS-stack planes variant
+#endif
+        if (planes && !perlin && (!p.counters || NRT_EXACT_PROF)) {  // KF_PLANES: the 4-wave f64 variant
             if (p.exact_wbvh && p.exact_pf && !p.exact_all) {  // the prefiltered world walk only
                 // (the world walk never reads the reference node array: not staged, 2.4 KB of
                 // LDS for the Cornell box)
@@ -166,6 +169,13 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                 if (vw.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
                     using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
                     const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+#if NRT_EXACT_PROF
+                    if (p.counters) {
+                        if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES | KF_PROF, XL>(p, vw, ring + stk + scene, stream);
+                        else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES | KF_PROF, XL>(p, vw, ring + stk, stream);
+                        return;
+                    }
+#endif
                     if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XL>(p, vw, ring + stk + scene, stream);
                     else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XL>(p, vw, ring + stk, stream);
                     return;
