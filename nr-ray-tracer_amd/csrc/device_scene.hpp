@@ -381,7 +381,11 @@ struct DSceneView {
     const DExactRef* wexact;  // f64 view: exact reference of each world-BVH slot (exact_wbvh mode)
     const DPrimWorld<float>* wxprims;  // f64 view: f32 world primitive of each of those slots (prefilter)
     uint32_t n_wexact;                 // slots of that tree
+    // f64 view: 4-wide nodes of that tree when the tree, wxprims and wexact are small enough to be
+    // staged in LDS with the scene (XSTAGE_MAX_BYTES; the Cornell box: 2 KB), else 0
+    uint32_t n_xstage;
 };
+constexpr uint32_t XSTAGE_MAX_BYTES = 8192;
 
 // World primitives staged in LDS sit 80 bytes apart (64-byte records + 16 bytes of padding): the
 // lanes of a ds_read_b128 group that read different records then start on different banks of
@@ -402,7 +406,10 @@ inline uint32_t lds_scene_bytes(const DSceneView<Real>& v, int maxd) {
            r16(v.n_xforms * sizeof(DXform<Real>)) + r16(v.n_instances * sizeof(DInstance)) +
            r16(v.n_materials * sizeof(DMaterial)) + r16(v.n_textures * sizeof(DTexture)) +
            r16(v.n_fprims * sizeof(DPrimFast<Real>)) + r16(v.n_inst_fast * sizeof(DInstFast<Real>)) +
-           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * wprim_lds_stride(maxd));
+           r16(v.n_mats_fast * sizeof(DMatFast)) + r16(v.n_wprims * wprim_lds_stride(maxd)) +
+           (v.n_xstage ? r16(v.n_xstage * sizeof(DBvh4cNode)) + r16(v.n_wexact * sizeof(DPrimWorld<float>)) +
+                             r16(v.n_wexact * sizeof(DExactRef))
+                       : 0u);
 }
 
 }  // namespace nrt

@@ -1996,7 +1996,9 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
 // The prefilter over the world-BVH walk (RenderParams::exact_pf).
 template <typename R, int MAXD, int W = 0, bool LSTACK = false>
 __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
-                                                    bool thread = false, uint16_t* lstk = nullptr) {
+                                                    bool thread = false, uint16_t* lstk = nullptr,
+                                                    unsigned long long* pc = nullptr, unsigned long long* tmid = nullptr) {
+    // (pc, tmid: PROF builds only -- walk events in the wave's profile row, the stamp before phase 2)
     static_assert(sizeof(R) == 8, "exact world-BVH mode is an f64-kernel mode");
     Ray<float> fr;
     fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
@@ -2005,8 +2007,10 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     c.init();
     auto offer_leaf = [&](int32_t ref, float& cut) {
         const uint32_t v = ~(uint32_t)ref, first = v >> 3, cnt = (v & 7u) + 1u;
-        for (uint32_t k = 0; k < cnt; ++k)
+        for (uint32_t k = 0; k < cnt; ++k) {
+            prof_event(pc, PROF_LEAF_TRIPS, PROF_LEAF_LANES);
             if (c.offer(load16(sc.wxprims + first + k), fr, first + k)) cut = c.bound * (1.0f + 0x1p-20f);
+        }
     };
     if (W == XTHREAD_W || (W == 0 && thread)) {
         float cut = INFINITY;
@@ -2036,7 +2040,10 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
             }
 #else
             while (true) {
-                while (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
+                while (ts.node >= 0) {
+                    prof_event(pc, PROF_VISIT_TRIPS, PROF_VISIT_LANES);
+                    wbvh4c_visit<R>(ts, sc, stk);
+                }
                 if (ts.node == WBVH_DONE) break;
                 offer_leaf(ts.node, ts.t_best);
                 ts.node = wbvh4c_pop(ts, stk);
@@ -2063,6 +2070,7 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
             ts.node = wbvh_pop(ts, stk);
         }
     }
+    if (tmid) *tmid = __builtin_amdgcn_s_memtime();
     if (c.over) return trace_exact_wbvh<R, MAXD, W, true, LSTACK>(sc, wray, hm, thread, lstk);
     return xcands_finish(c, sc, wray, hm);
 }
@@ -2168,7 +2176,8 @@ __device__ __forceinline__ bool trace_exact_slots(const DSceneView<R>& sc, const
 template <typename R, int MAXD, bool EXACT, bool FLAT = false, bool PF = false, class SIG = NoSig, class STKP>
 __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wray, HitMin<R, MAXD>& hm,
                                       STKP stack, bool all = false, bool exact_wbvh = false, uint32_t pf = 0,
-                                      bool xthread = false) {
+                                      bool xthread = false, unsigned long long* pc = nullptr,
+                                      unsigned long long* tmid = nullptr) {
     if constexpr (MAXD == 0) return trace_world<R, MAXD, FLAT, SIG>(sc, wray, hm);
     else if constexpr (MAXD < 0) return trace_world_bvh<R, MAXD, FLAT, SIG>(sc, wray, hm, stack);
     else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_SLOTS) return trace_exact_slots<R, MAXD>(sc, wray, hm);
@@ -2177,7 +2186,7 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
         return trace_exact_slots_pf<R, MAXD>(sc, wray, hm);
     } else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
         static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
-        if constexpr (SIG::lstack) return trace_exact_wbvh_pf<R, MAXD, SIG::bvh, true>(sc, wray, hm, false, stack);
+        if constexpr (SIG::lstack) return trace_exact_wbvh_pf<R, MAXD, SIG::bvh, true>(sc, wray, hm, false, stack, pc, tmid);
         else return trace_exact_wbvh_pf<R, MAXD, SIG::bvh>(sc, wray, hm);
     } else if constexpr (EXACT && sizeof(R) == 8) {
         const bool thread = sc.xthread != nullptr && xthread;
@@ -2541,6 +2550,13 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
         for (uint32_t k = threadIdx.x; k < g.n_wprims * Q; k += BLOCK) ((uint4*)dst)[(k / Q) * QS + k % Q] = s4[k];
         off += (g.n_wprims * wstride + 15u) & ~15u;
         s.wprims = (const DPrimWorld<R>*)dst;
+    }
+    if constexpr (sizeof(R) == 8) {  // small culling trees of the exact world walk (DSceneView::n_xstage)
+        if (g.n_xstage) {
+            s.wbvh4c = (const DBvh4cNode*)copy(g.wbvh4c, g.n_xstage * (uint32_t)sizeof(DBvh4cNode));
+            s.wxprims = (const DPrimWorld<float>*)copy(g.wxprims, g.n_wexact * (uint32_t)sizeof(DPrimWorld<float>));
+            s.wexact = (const DExactRef*)copy(g.wexact, g.n_wexact * (uint32_t)sizeof(DExactRef));
+        }
     }
     __syncthreads();
     return s;
@@ -3139,7 +3155,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     fresh = false;
                 }
                 const unsigned long long t1 = stamp();
-                unsigned long long t2 = t1;
+                unsigned long long t2 = t1, tmid = 0;
                 HitMin<R, MAXD> hm;
                 bool hit = false;
                 const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
@@ -3147,8 +3163,11 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     // world list: the global tables through the scalar cache; records read LDS
                     hit = trace<R, MAXD, EXACT, FLAT, (KFLAGS & KF_PLANES) != 0, SIG>(
                         MAXD == 0 ? gsc : sc, ray, hm, stack, p.exact_all != 0, p.exact_wbvh != 0, p.exact_pf,
-                        p.exact_thread != 0);
+                        p.exact_thread != 0, PROF ? prof[wave] : nullptr, PROF ? &tmid : nullptr);
                     t2 = stamp();
+                    if constexpr (PROF) {
+                        if (leader() && tmid) atomicAdd(&prof[wave][6], t2 - tmid);  // phase 2 (f64 candidate tests)
+                    }
                 }
                 if constexpr (NRT_EXACT_SETPRIO > 0) __builtin_amdgcn_s_setprio(NRT_EXACT_SETPRIO);
                 fresh = !shade(traced, hit, hm);

@@ -138,6 +138,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
             // (the reference node array is never read: not staged)
             DSceneView<R> vw = v;
             vw.n_nodes = 0;
+            vw.n_xstage = 0;  // (no walk)
             const uint32_t scene = lds_scene_bytes(vw, MAXD);
             using XS = dev::ExactSig<dev::EXACT_SIG_SLOTS, 0>;
             if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, 0, XS>(p, vw, ring + scene, stream);
@@ -161,6 +162,9 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                     return;
                 }
                 if (p.exact_slots && vw.n_wexact <= dev::EXACT_SLOTS_MAX) {  // small scenes: every slot, no walk
+                    // (the slot records arrive by scalar loads from global memory: not staged)
+                    vw.n_xstage = 0;
+                    const uint32_t scene = lds_scene_bytes(vw, MAXD);
                     using XA = dev::ExactSig<dev::EXACT_SIG_SLOTS_PF, 0>;
                     if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XA>(p, vw, ring + scene, stream);
                     else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XA>(p, vw, ring, stream);

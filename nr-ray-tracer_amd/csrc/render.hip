@@ -162,7 +162,14 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                      wx_ok ? (uint32_t)xt.nodes.size() : 0u,
                                      std::max<uint32_t>(1u, x4 ? xt.stack4 : xt.depth), wx_ok ? xth : nullptr,
                                      wx_ok ? xt.threaded_n : 0u, wx_ok ? wx : nullptr,
-                                     wx_ok ? wxp : nullptr, wx_ok ? (uint32_t)fs.wexact.size() : 0u};
+                                     wx_ok ? wxp : nullptr, wx_ok ? (uint32_t)fs.wexact.size() : 0u, 0u};
+        {  // small culling trees travel into LDS with the scene (knob NRT_EXACT_XSTAGE=0: read from HBM)
+            const size_t xb = xt.nodes4c.size() * sizeof(DBvh4cNode) +
+                              fs.wexact.size() * (sizeof(DPrimWorld<float>) + sizeof(DExactRef));
+            const char* xs = std::getenv("NRT_EXACT_XSTAGE");
+            if (wx_ok && x4 && x4c && xb <= XSTAGE_MAX_BYTES && !(xs && xs[0] == '0'))
+                ds->v64.n_xstage = (uint32_t)xt.nodes4c.size();
+        }
         // the fast kernel reads fast prims only: no f32 DPrim copy in its LDS image
         ds->v32 = DSceneView<float>{n32, p32, x32, inst, mats, texs, texels, fs.root_fast, fs.max_depth,
                                     (uint32_t)f32.nodes.size(), 0, 0, ni, nm, nt, fpr, ifast, mfast,
@@ -170,7 +177,7 @@ DeviceScene* gpu_upload_scene(const FlatScene& fs, int device) {
                                     (uint32_t)fs.mats_fast.size(), wpr, (uint32_t)f32.wprims.size(), wrn,
                                     (uint32_t)fs.wruns.size(), fs.wflags, wbn, use_wbvh4(fs) ? wb4 : nullptr,
                                     use_wbvh4(fs) ? wb4c : nullptr, fs.wbvh.root4, fs.wbvh.root,
-                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, 0u, nullptr, nullptr, 0u};
+                                    (uint32_t)fs.wbvh.nodes.size(), wstack, nullptr, 0u, nullptr, nullptr, 0u, 0u};
         ds->wbvh_ok = fs.wbvh_ok && fs.wbvh_f32_ok;  // (the f32 world-BVH modes)
         for (const DTexture& t : fs.textures) ds->perlin |= t.kind == TEX_NOISE || t.kind == TEX_MARBLE;
         ds->planes = !fs.prims.empty();
