@@ -75,6 +75,9 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_CHACHA_FAKE
 #define NRT_CHACHA_FAKE 0  // attribution builds: ChaCha8 blocks replaced by a cheap hash (frames differ)
 #endif
+#ifndef XWALK_WAIT
+#define XWALK_WAIT 40  // persistent exact walk: lanes done walking before a shading round (host default: launch_impl.hpp)
+#endif
 #ifndef NRT_RIUS_WAVE
 #define NRT_RIUS_WAVE 1  // ChaCha8 rejection samplers as wave-converged loops (rejection_wave; see render_kernel)
 #endif
@@ -1030,6 +1033,7 @@ struct NoSig {
     static constexpr int prims = 0;  // world-BVH leaf primitive kinds (WPRIMS_*), 0: decided per primitive
     static constexpr int exact = 0;  // exact kernel: traversal fixed at compile time (ExactSig), 0: runtime
     static constexpr bool lstack = false;
+    static constexpr bool persist = false;
 };
 template <uint32_t... RUNS>
 struct WorldSig {
@@ -1039,12 +1043,13 @@ struct WorldSig {
     static constexpr int prims = 0;
     static constexpr int exact = 0;
     static constexpr bool lstack = false;
+    static constexpr bool persist = false;
 };
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
 // the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
 // plane-only scenes, and the unfiltered walk it falls back to).
 enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2, EXACT_SIG_SLOTS = 3 };
-template <int MODE, int WIDTH, bool LSTACK = false>
+template <int MODE, int WIDTH, bool LSTACK = false, bool PERSIST = false>
 struct ExactSig {
     static constexpr uint32_t n = 0;
     static constexpr int bvh = WIDTH;  // culling walk: 4 / 2 the stack walk of that width, XTHREAD_W the
@@ -1053,6 +1058,8 @@ struct ExactSig {
     static constexpr int prims = 0;
     static constexpr int exact = MODE;
     static constexpr bool lstack = LSTACK;  // compact walk: its 16-bit stack in LDS (fewer waves), not scratch
+    // the prefiltered compact walk kept across shading rounds (XWalk; render_kernel's persistent-walk loop)
+    static constexpr bool persist = PERSIST;
 };
 // World-BVH mode (jit.hip): the tree's width (2 or 4), whether it holds coplanar-tie keys
 // (WFLAG_COPLANAR) and which primitive kinds its leaves hold (WPRIMS_*) as constants, so one
@@ -1065,6 +1072,7 @@ struct BvhSig {
     static constexpr int prims = PRIMS;
     static constexpr int exact = 0;
     static constexpr bool lstack = false;
+    static constexpr bool persist = false;
 };
 template <bool FLAT, uint32_t... RUNS>
 __device__ __forceinline__ void sig_runs(WorldSig<RUNS...>, ConstPrimWorld<float> wp, uint32_t& k, const Ray<float>& ray,
@@ -2073,6 +2081,48 @@ __device__ __forceinline__ bool trace_exact_wbvh_pf(const DSceneView<R>& sc, con
     if (tmid) *tmid = __builtin_amdgcn_s_memtime();
     if (c.over) return trace_exact_wbvh<R, MAXD, W, true, LSTACK>(sc, wray, hm, thread, lstk);
     return xcands_finish(c, sc, wray, hm);
+}
+
+// The prefiltered compact walk as a resumable state (ExactSig PERSIST): the kernel advances the
+// walks of its lanes one trip at a time and shades the lanes whose walk has ended once enough of
+// them have (render_kernel), so lanes that finish early start their next segment instead of idling
+// behind the wave's longest walk.  A trip offers one primitive of the parked leaf, visits one node,
+// and parks the next leaf the visit or a pop reaches.  The candidates, their bounds and the winner
+// are those of trace_exact_wbvh_pf: a leaf's primitives are offered in the same order, and the cut
+// a certain hit sets only prunes.
+struct XWalk {
+    WbvhTrav ts;  // (ts.leaf: the parked leaf cursor ~(first << 3 | more))
+    XCands c;
+    Ray<float> fr;
+    __device__ __forceinline__ bool busy() const { return ts.busy(); }
+};
+template <typename R>
+__device__ __forceinline__ void xwalk_begin(XWalk& w, const DSceneView<R>& sc, const Ray<R>& wray, bool query) {
+    w.fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    w.fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    w.c.init();
+    wbvh_begin(w.ts, query ? wbvh_root(sc) : WBVH_DONE, w.fr);  // depth cap: no query (Q6)
+}
+template <typename R, class STK>
+__device__ __forceinline__ void xwalk_trip(XWalk& w, const DSceneView<R>& sc, STK& stk) {
+    WbvhTrav& ts = w.ts;
+    if (ts.leaf != WBVH_NO_LEAF) {
+        const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
+        if (w.c.offer(load16(sc.wxprims + first), w.fr, first)) ts.t_best = w.c.bound * (1.0f + 0x1p-20f);
+        ts.leaf = more ? ts.leaf - 7 : WBVH_NO_LEAF;  // ~((first + 1) << 3 | (more - 1)) = ~v - 7
+    }
+    if (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
+    if (ts.leaf == WBVH_NO_LEAF && ts.node < 0 && ts.node != WBVH_DONE) {
+        ts.leaf = ts.node;
+        ts.node = wbvh4c_pop(ts, stk);
+    }
+}
+// the walk has ended: phase 2 (or, after a candidate overflow, the unfiltered walk)
+template <typename R, int MAXD, class STK>
+__device__ __forceinline__ bool xwalk_finish(const XWalk& w, const DSceneView<R>& sc, const Ray<R>& wray,
+                                             HitMin<R, MAXD>& hm, STK& stk) {
+    if (w.c.over) return trace_exact_wbvh<R, MAXD, WBVH_COMPACT, true, true>(sc, wray, hm, false, stk);
+    return xcands_finish(w.c, sc, wray, hm);
 }
 
 // Small plane-only scenes (at most EXACT_SLOTS_MAX slots, EXACT_SIG_SLOTS_PF): the prefilter over
@@ -3132,6 +3182,60 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     begin();
                 }
                 if (__ballot(active) == 0ull) break;
+            }
+        } else if constexpr (SIG::persist) {
+            // Exact world walk kept across shading rounds (XWalk): the wave runs walk trips until a
+            // ballot shows p.wave_wait lanes (default XWALK_WAIT) done, then those lanes run the
+            // candidate tests, shade and begin their next segment, as the f32 world-BVH loop above.
+            static_assert(EXACT && sizeof(R) == 8 && SIG::lstack, "persistent exact walk: f64, LDS stack");
+            XWalk xw;
+            xw.ts.node = WBVH_DONE;
+            xw.ts.leaf = WBVH_NO_LEAF;
+            bool active = false;
+            bool want = have;  // the lane starts its pixel's next sample (one camera_ray call site)
+            auto begin = [&]() { xwalk_begin(xw, sc, ray, b < p.max_bounces); };
+            const uint32_t wait_min = p.wave_wait ? p.wave_wait : (uint32_t)XWALK_WAIT;
+            while (true) {
+                if (want) {
+                    active = camera_ray();  // (s < spp)
+                    begin();
+                    want = false;
+                }
+                const unsigned long long t0 = stamp();
+                const uint64_t am = __ballot(active);
+                while (true) {
+                    const bool going = active && xw.busy();
+                    const uint64_t gm = __ballot(going);
+                    if (gm == 0ull || (uint32_t)__popcll(am & ~gm) >= wait_min) break;
+                    if (going) xwalk_trip<R>(xw, sc, stack);
+                }
+                const unsigned long long t1 = stamp();
+                if (active && !xw.busy()) {
+                    HitMin<R, MAXD> hm;
+                    const bool traced = b < p.max_bounces;  // depth cap returns black (Q6)
+                    const bool hit = traced && xwalk_finish<R, MAXD>(xw, sc, ray, hm, stack);
+                    if (shade(traced, hit, hm)) {
+                        begin();
+                    } else {
+                        active = false;
+                        want = s < p.spp;
+                    }
+                }
+                if constexpr (PROF) {
+                    const unsigned long long t2 = stamp();
+                    if (leader()) {
+                        atomicAdd(&prof[wave][0], 1ull);
+                        atomicAdd(&prof[wave][2], t1 - t0);
+                        atomicAdd(&prof[wave][3], t2 - t1);
+                    }
+                }
+                if (have && !active && !want) {  // the pixel's last sample has ended
+                    finish_pixel();
+                    have = false;
+                }
+                flush_claims();
+                if (next_pixel(!have)) want = true;
+                if (__ballot(active || want) == 0ull) break;
             }
         } else {
             bool fresh = true;

@@ -173,6 +173,29 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                 if (vw.wbvh4c && p.exact_lstack) {  // the compact walk's stack in LDS, 3 waves per SIMD
                     using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
                     const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+                    // the walk kept across shading rounds (XWalk; knob NRT_EXACT_PERSIST=0: one walk per segment)
+                    static const bool persist = [] {
+                        const char* e = std::getenv("NRT_EXACT_PERSIST");
+                        return !(e && e[0] == '0');
+                    }();
+                    if (persist) {
+                        using XP = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true, true>;
+                        // shading rounds at 40 walks done (the teapot: 40 / 48 / 64 measured 132 / 132-133 /
+                        // 147 ms, 16 / 32 164 / 145 ms, one walk per segment 169 ms); small staged trees (the
+                        // Cornell box: short walks) at 64, a while-while walk in trips (182 vs 186 ms; 48: 190)
+                        RenderParams q = p;
+                        if (!q.wave_wait) q.wave_wait = vw.n_xstage ? 64u : 40u;
+#if NRT_EXACT_PROF
+                        if (q.counters) {
+                            if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES | KF_PROF, XP>(q, vw, ring + stk + scene, stream);
+                            else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES | KF_PROF, XP>(q, vw, ring + stk, stream);
+                            return;
+                        }
+#endif
+                        if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES, XP>(q, vw, ring + stk + scene, stream);
+                        else launch_variant<R, G, MAXD, EXACT, false, dev::KF_PLANES, XP>(q, vw, ring + stk, stream);
+                        return;
+                    }
 #if NRT_EXACT_PROF
                     if (p.counters) {
                         if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, dev::KF_PLANES | KF_PROF, XL>(p, vw, ring + stk + scene, stream);
