@@ -1848,7 +1848,10 @@ __device__ __forceinline__ bool trace_exact_wbvh(const DSceneView<R>& sc, const 
 // (smallest exact t, ties to the higher depth-first rank, as trace_exact_wbvh).  Boxes are cut
 // at the bound raised by 2^-20 as there.  A lane with more than XCAND live candidates at once
 // (never seen on the reference scenes) falls back to trace_exact_wbvh.
-constexpr int XCAND = 4;
+#ifndef NRT_XCAND
+#define NRT_XCAND 2  // live candidates per ray (2 / 3 / 4: C5 f64 179.9 / 180.4 / 182.5 ms, C4 133.0 / 133.5 / 136.4)
+#endif
+constexpr int XCAND = NRT_XCAND;
 #ifndef NRT_PF_RCP
 #define NRT_PF_RCP 1
 #endif
