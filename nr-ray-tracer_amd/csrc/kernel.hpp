@@ -78,6 +78,9 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef XWALK_WAIT
 #define XWALK_WAIT 40  // persistent exact walk: lanes done walking before a shading round (host default: launch_impl.hpp)
 #endif
+#ifndef NRT_REC_CARRY
+#define NRT_REC_CARRY 1  // the exact hit record reuses the winner's plane-test values (HitMin::pre)
+#endif
 #ifndef NRT_RIUS_WAVE
 #define NRT_RIUS_WAVE 1  // ChaCha8 rejection samplers as wave-converged loops (rejection_wave; see render_kernel)
 #endif
@@ -627,9 +630,11 @@ __device__ __forceinline__ R sphere_t(const DPrim<R>& s, const Ray<R>& r) {
 
 // Plane::hit (plane.rs:141-174) with range [0.001, inf]; t or -1; alpha/beta out.
 template <typename R>
-__device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alpha, R& beta, V<R>& point) {
+__device__ __forceinline__ R plane_t(const DPrim<R>& q, const Ray<R>& r, R& alpha, R& beta, V<R>& point,
+                                     R* den_out = nullptr) {
     const V<R> nrm = ld3(q.n);
     const R denom = dot(nrm, r.d);
+    if (den_out) *den_out = denom;
     if (fabs(denom) < R(1e-8)) return R(-1);
     const R t = fast_div(q.s - dot(nrm, r.o), denom);
     if (!(R(0.001) <= t && t <= R(INFINITY))) return R(-1);
@@ -840,6 +845,11 @@ struct HitMin {
     uint32_t prim;
     int depth;
     uint32_t inst[MAXD > 0 ? MAXD : 1];
+    // the exact plane test's own object-space point, (alpha, beta) and n.d of the winner, which the
+    // hit record would compute again bit for bit (xcands_finish, NRT_REC_CARRY); pre: they are set
+    V<R> pp;
+    R pu, pv, pden;
+    bool pre = false;
 };
 
 // World-space mode (MAXD = 0, fast kernel): the wave tests every primitive,
@@ -1986,14 +1996,20 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
                 if (ref.inst >= 0) xform_in<R, true, false>(sc, sc.instances[ref.inst], oray);
                 cur_inst = ref.inst;
             }
-            R alpha, beta;
+            R alpha, beta, den;
             V<R> point;
-            const R t = plane_t(sc.prims[ref.prim], oray, alpha, beta, point);
+            const R t = plane_t(sc.prims[ref.prim], oray, alpha, beta, point, &den);
             if (t >= R(0) && (t < best_t || (t == best_t && ref.rank > best_rank))) {
                 best_t = t;
                 best_rank = ref.rank;
                 best_prim = (int32_t)ref.prim;
                 best_inst = ref.inst;
+                if constexpr (NRT_REC_CARRY) {
+                    hm.pp = point;
+                    hm.pu = alpha;
+                    hm.pv = beta;
+                    hm.pden = den;
+                }
             }
         }
     }
@@ -2001,6 +2017,7 @@ __device__ __forceinline__ bool xcands_finish(const XCands& c, const DSceneView<
     hm.prim = (uint32_t)best_prim;
     hm.depth = best_inst >= 0 ? 1 : 0;
     hm.inst[0] = (uint32_t)best_inst;
+    hm.pre = NRT_REC_CARRY != 0;
     return best_prim >= 0;
 }
 
@@ -2327,8 +2344,9 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
         if constexpr (EXACT) xform_out(sc, sc.instances[iid], rec);
         else leave_fast(sc.inst_fast[iid], rec);
     };
+    const bool pre = EXACT && PLANES && NRT_REC_CARRY && hm.pre;  // (xcands_finish: object-space values carried)
     if constexpr (MAXD == 1) {
-        if (hm.depth > 0) enter(hm.inst[0]);
+        if (hm.depth > 0 && !pre) enter(hm.inst[0]);
     } else {
         for (int l = 0; l < hm.depth; ++l) enter(hm.inst[l]);
     }
@@ -2370,6 +2388,11 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
             h.u = phi / (R(2.0) * R(M_PI));
             h.v = theta / R(M_PI);
         }
+    } else if (pre) {  // the same point, (alpha, beta) and n.d as plane_t computed them
+        h.p = hm.pp;
+        h.u = hm.pu;
+        h.v = hm.pv;
+        outward = ld3(pr.n);
     } else {  // plane.rs:156-159
         h.p = vfma(t, ray.d, ray.o);
         const V<R> ph = h.p - ld3(pr.a);
@@ -2377,8 +2400,8 @@ __device__ __forceinline__ Rec<R> make_record_bvh(const DSceneView<R>& sc, const
         h.v = dot(ld3(pr.w), cross(ld3(pr.b), ph));
         outward = ld3(pr.n);
     }
-    // HitRecord::new_with_uv (hitable.rs:38-59)
-    const R sign = signum(dot(ray.d, outward));
+    // HitRecord::new_with_uv (hitable.rs:38-59) (n.d = d.n: the products commute)
+    const R sign = signum(pre ? hm.pden : dot(ray.d, outward));
     h.front = sign < R(0);
     h.n = (-sign) * outward;
     if constexpr (EXACT) h.mat = pr.material;
