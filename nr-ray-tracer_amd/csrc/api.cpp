@@ -794,6 +794,8 @@ int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count
     return guarded(NRT_E_DEVICE, [&]() {
         if (!out && lanes && count) throw std::invalid_argument("null output");
         if (rng > RNG_PHILOX2_BLOCK) throw std::invalid_argument("unknown rng");
+        if (rng == RNG_CHACHA8 && stream0 + lanes > 0xFFFFFFFFull)  // (pixel streams: make_params caps images below 2^32 pixels)
+            throw std::invalid_argument("ChaCha8 probe: streams are pixel indices below 2^32");
         if (rng == RNG_PHILOX2_BLOCK && (count > PHILOX2_STEPS || stream0 + lanes > 0xFFFFFFFFull || sample >= PHILOX2_MAX_SPP))
             throw std::invalid_argument("Philox2x32 block probe: step, pixel or sample out of range");
         gpu_rng_probe(rng, stream0, lanes, count, sample, out);

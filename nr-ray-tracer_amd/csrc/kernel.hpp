@@ -225,15 +225,17 @@ __device__ __forceinline__ void chacha8_block(uint32_t ctr_lo, uint32_t ctr_hi, 
 // Refills are batched per wave: when any active lane is empty, every active
 // lane with room for a block generates one, so a wave computes about one
 // block per 8-9 draw steps even when lanes have drifted apart.
+// The stream is the pixel index, below 2^32 (make_params caps images below 2^32 pixels; the probe
+// checks its range), so the stream's high word is the constant 0 and two of the first column
+// round's quarter rounds fold to constants (6 % of a block's operations).
 struct ChaCha8 {
     static constexpr bool uses_lds = true;
     static constexpr bool exact_stream = true;  // draws must follow the reference's sequence
-    uint32_t s_lo, s_hi, ctr, head, count;
+    uint32_t s_lo, ctr, head, count;
     uint2* ring;  // slot k of this lane at ring[k * BLOCK]
 
     __device__ __forceinline__ void init(uint64_t stream, uint2* base) {
         s_lo = (uint32_t)stream;
-        s_hi = (uint32_t)(stream >> 32);
         ctr = 0;
         head = 0;
         count = 0;
@@ -246,7 +248,7 @@ struct ChaCha8 {
 #pragma unroll
         for (int k = 0; k < 16; ++k) w[k] = (ctr * 16u + (uint32_t)k) * 0x9E3779B9u ^ s_lo;
 #else
-        chacha8_block(ctr, 0u, s_lo, s_hi, w);
+        chacha8_block(ctr, 0u, s_lo, 0u, w);
 #endif
         ++ctr;
         uint32_t slot = (head + count) & (RING - 1);

@@ -211,3 +211,12 @@ def test_render_argument_errors_are_invalid():
     with pytest.raises(nrt.NrtError) as ei:
         scene.render(cam, precision="f32", rng="philox", device=10 ** 6)
     assert ei.value.code in (-1, -3)  # device ordinal out of range (-1), or no GPU at all (-3)
+
+
+def test_chacha8_probe_streams_below_2_32():
+    """ChaCha8 streams are pixel indices, below 2^32 (images are capped below 2^32 pixels, and the
+    kernels fold the stream's zero high word): the probe refuses streams past that before any device
+    work, whether or not a GPU is present."""
+    with pytest.raises(nrt.NrtError) as ei:
+        nrt.debug_rng("chacha8", 2 ** 32 - 8, 64, 4)
+    assert ei.value.code == -1 and "2^32" in str(ei.value)
