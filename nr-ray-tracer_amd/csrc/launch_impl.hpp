@@ -174,10 +174,8 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                     using XL = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true>;
                     const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
                     // the walk kept across shading rounds (XWalk; knob NRT_EXACT_PERSIST=0: one walk per segment)
-                    static const bool persist = [] {
-                        const char* e = std::getenv("NRT_EXACT_PERSIST");
-                        return !(e && e[0] == '0');
-                    }();
+                    const char* pe = std::getenv("NRT_EXACT_PERSIST");
+                    const bool persist = !(pe && pe[0] == '0');
                     if (persist) {
                         using XP = dev::ExactSig<dev::EXACT_SIG_WORLD_PF, WBVH_COMPACT, true, true>;
                         // shading rounds at 40 walks done (the teapot: 40 / 48 / 64 measured 132 / 132-133 /

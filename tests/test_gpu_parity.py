@@ -298,9 +298,15 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
     # entries, in scratch or, with NRT_EXACT_LSTACK, in LDS at 3 waves per SIMD); small scenes can
     # visit every slot in order instead of walking (NRT_EXACT_SLOTS): plane-only scenes through the
     # prefilter, scenes with spheres with the reference tests alone (EXACT_SIG_SLOTS)
-    modes = {"bvh": ("0", "0", "0", "0", "0"), "all": ("1", "0", "0", "0", "0"), "world": ("0", "1", "0", "0", "0"),
-             "world_pf": ("0", "1", "1", "0", "0"), "world_pf_lds_stack": ("0", "1", "1", "1", "0"),
-             "world_pf_slots": ("0", "1", "1", "1", "1")}
+    # With the LDS stack the prefiltered walk is kept across shading rounds by default (XWalk,
+    # NRT_EXACT_PERSIST; shading rounds at NRT_WAVE_WAIT walks done): one walk per segment and a
+    # round per finished lane must give the same frame.
+    modes = {"bvh": ("0", "0", "0", "0", "0", "1", "0"), "all": ("1", "0", "0", "0", "0", "1", "0"),
+             "world": ("0", "1", "0", "0", "0", "1", "0"), "world_pf": ("0", "1", "1", "0", "0", "1", "0"),
+             "world_pf_lds_stack": ("0", "1", "1", "1", "0", "1", "0"),
+             "world_pf_lds_stack_one_walk": ("0", "1", "1", "1", "0", "0", "0"),
+             "world_pf_lds_stack_wait1": ("0", "1", "1", "1", "0", "1", "1"),
+             "world_pf_slots": ("0", "1", "1", "1", "1", "1", "0")}
     for name, env in modes.items():
         if name.startswith("world") and s.stats()["exact_mode"] != 2:
             continue
@@ -309,7 +315,16 @@ def test_exact_modes_bitwise_identical(scene, w, h, spp, monkeypatch):
         monkeypatch.setenv("NRT_EXACT_PF", env[2])
         monkeypatch.setenv("NRT_EXACT_LSTACK", env[3])
         monkeypatch.setenv("NRT_EXACT_SLOTS", env[4])
+        monkeypatch.setenv("NRT_EXACT_PERSIST", env[5])
+        monkeypatch.setenv("NRT_WAVE_WAIT", env[6])
         frames[name] = s.render(precision="f64", rng="chacha8")
+    monkeypatch.setenv("NRT_WAVE_WAIT", "0")
+    monkeypatch.setenv("NRT_EXACT_PERSIST", "1")
+    if s.stats()["exact_mode"] == 2:  # the culling tree read from global memory, not staged in LDS
+        monkeypatch.setenv("NRT_EXACT_XSTAGE", "0")  # (read at upload: a fresh scene)
+        monkeypatch.setenv("NRT_EXACT_SLOTS", "0")
+        frames["world_pf_global_tree"] = load(scene, w, h, spp).render(precision="f64", rng="chacha8")
+        monkeypatch.setenv("NRT_EXACT_XSTAGE", "1")
     if s.stats()["exact_mode"] == 2:  # the 4-wide tree with 32-bit refs (NRT_EXACT_COMPACT=0, read at upload)
         monkeypatch.setenv("NRT_EXACT_COMPACT", "0")
         monkeypatch.setenv("NRT_EXACT_LSTACK", "0")
