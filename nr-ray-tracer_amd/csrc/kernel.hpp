@@ -72,9 +72,6 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_CAM_RELOAD
 #define NRT_CAM_RELOAD 0  // f32 camera vectors: scalar loads from the kernel arguments at the use
 #endif
-#ifndef NRT_CHACHA_FAKE
-#define NRT_CHACHA_FAKE 0  // attribution builds: ChaCha8 blocks replaced by a cheap hash (frames differ)
-#endif
 #ifndef XWALK_WAIT
 #define XWALK_WAIT 40  // persistent exact walk: lanes done walking before a shading round (host default: launch_impl.hpp)
 #endif
@@ -244,12 +241,7 @@ struct ChaCha8 {
     __device__ __forceinline__ void start_sample(uint32_t) {}
     __device__ __forceinline__ void refill() {
         uint32_t w[16];
-#if NRT_CHACHA_FAKE  // attribution builds only (not the reference stream): a cheap stand-in for the block
-#pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = (ctr * 16u + (uint32_t)k) * 0x9E3779B9u ^ s_lo;
-#else
         chacha8_block(ctr, 0u, s_lo, 0u, w);
-#endif
         ++ctr;
         uint32_t slot = (head + count) & (RING - 1);
 #pragma unroll
