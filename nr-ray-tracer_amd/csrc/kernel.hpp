@@ -1052,7 +1052,8 @@ struct WorldSig {
 // Exact f64 kernel: the traversal nrt_exact_mode picked, as a constant, so the variant carries
 // the code of that walk only (EXACT_SIG_WORLD_PF: the world-BVH walk with the f32 prefilter of
 // plane-only scenes, and the unfiltered walk it falls back to).
-enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2, EXACT_SIG_SLOTS = 3 };
+enum : int { EXACT_SIG_WORLD_PF = 1, EXACT_SIG_SLOTS_PF = 2, EXACT_SIG_SLOTS = 3, EXACT_SIG_WORLD = 4 };
+// (EXACT_SIG_WORLD: the unfiltered world walk of scenes with spheres, compact tree, LDS stack)
 template <int MODE, int WIDTH, bool LSTACK = false, bool PERSIST = false>
 struct ExactSig {
     static constexpr uint32_t n = 0;
@@ -2248,6 +2249,9 @@ __device__ __forceinline__ bool trace(const DSceneView<R>& sc, const Ray<R>& wra
     else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_SLOTS_PF) {
         static_assert(PF, "EXACT_SIG_SLOTS_PF is a KF_PLANES variant");
         return trace_exact_slots_pf<R, MAXD>(sc, wray, hm);
+    } else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD) {
+        static_assert(SIG::lstack && SIG::bvh == WBVH_COMPACT, "EXACT_SIG_WORLD: the compact walk, LDS stack");
+        return trace_exact_wbvh<R, MAXD, WBVH_COMPACT, PF, true>(sc, wray, hm, false, stack);
     } else if constexpr (EXACT && sizeof(R) == 8 && SIG::exact == EXACT_SIG_WORLD_PF) {
         static_assert(PF, "EXACT_SIG_WORLD_PF is a KF_PLANES variant");
         if constexpr (SIG::lstack) return trace_exact_wbvh_pf<R, MAXD, SIG::bvh, true>(sc, wray, hm, false, stack, pc, tmid);

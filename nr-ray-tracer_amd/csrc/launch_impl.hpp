@@ -148,6 +148,19 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
 #ifndef NRT_EXACT_PROF
 #define NRT_EXACT_PROF 0  // diagnostic builds: the phase profile (p.counters) of the LDS-stack planes variant
 #endif
+        if (!planes && !perlin && !p.counters && p.exact_wbvh && !p.exact_all && !p.exact_thread && v.wbvh4c &&
+            p.exact_lstack && !(p.exact_slots && v.n_wexact <= dev::EXACT_SLOTS_MAX)) {
+            // larger scenes with spheres (spheres.toml): the unfiltered world walk on the compact tree with
+            // its stack in LDS (the generic kernel's walk keeps a 32-bit stack in scratch)
+            using XW = dev::ExactSig<dev::EXACT_SIG_WORLD, WBVH_COMPACT, true>;
+            DSceneView<R> vw = v;
+            vw.n_nodes = 0;  // (the world walk never reads the reference node array)
+            const uint32_t scene = lds_scene_bytes(vw, MAXD);
+            const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+            if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, 0, XW>(p, vw, ring + stk + scene, stream);
+            else launch_variant<R, G, MAXD, EXACT, false, 0, XW>(p, vw, ring + stk, stream);
+            return;
+        }
         if (planes && !perlin && (!p.counters || NRT_EXACT_PROF)) {  // KF_PLANES: the 4-wave f64 variant
             if (p.exact_wbvh && p.exact_pf && !p.exact_all) {  // the prefiltered world walk only
                 // (the world walk never reads the reference node array: not staged, 2.4 KB of
