@@ -2140,6 +2140,79 @@ __device__ __forceinline__ bool xwalk_finish(const XWalk& w, const DSceneView<R>
     return xcands_finish(w.c, sc, wray, hm);
 }
 
+template <bool B, class T, class F> struct TypeIf { using type = T; };  // (hiprtc: no <type_traits>)
+template <class T, class F> struct TypeIf<false, T, F> { using type = F; };
+// The unfiltered world walk (EXACT_SIG_WORLD: scenes with spheres) as a resumable state, for the
+// same persistent loop: a trip runs the reference test (Sphere::hit / Plane::hit in f64 in the
+// primitive's object space, sphere.rs:105-163, plane.rs:141-174) on the parked leaf's next
+// primitive and visits one node; the winner is trace_exact_wbvh's (smallest t, ties to the higher
+// depth-first rank, object.rs:109-115), and the cut it sets only prunes.
+template <typename R>
+struct XWalkU {
+    WbvhTrav ts;
+    Ray<float> fr;
+    R best_t;
+    uint32_t best_rank;
+    int32_t best_prim, best_inst;
+    __device__ __forceinline__ bool busy() const { return ts.busy(); }
+};
+template <typename R>
+__device__ __forceinline__ void xwalk_begin(XWalkU<R>& w, const DSceneView<R>& sc, const Ray<R>& wray, bool query) {
+    w.fr.o = mk((float)wray.o.x, (float)wray.o.y, (float)wray.o.z);
+    w.fr.d = mk((float)wray.d.x, (float)wray.d.y, (float)wray.d.z);
+    w.best_t = R(INFINITY);
+    w.best_rank = 0;
+    w.best_prim = -1;
+    w.best_inst = -1;
+    wbvh_begin(w.ts, query ? wbvh_root(sc) : WBVH_DONE, w.fr);
+}
+template <typename R, class STK>
+__device__ __forceinline__ void xwalk_trip(XWalkU<R>& w, const DSceneView<R>& sc, STK& stk, const Ray<R>& wray) {
+    WbvhTrav& ts = w.ts;
+    if (ts.leaf != WBVH_NO_LEAF) {
+        const uint32_t v = ~(uint32_t)ts.leaf, first = v >> 3, more = v & 7u;
+        const DExactRef rf = sc.wexact[first];
+        Ray<R> oray = wray;  // the primitive's object-space ray (exact chain)
+        if (rf.inst >= 0) xform_in<R, true, false>(sc, sc.instances[rf.inst], oray);
+        const DPrim<R>& pr = sc.prims[rf.prim];
+        R t;
+        if (pr.kind == PRIM_SPHERE) {
+            t = sphere_t(pr, oray);
+        } else {
+            R alpha, beta;
+            V<R> point;
+            t = plane_t(pr, oray, alpha, beta, point);
+        }
+        if (t >= R(0) && (t < w.best_t || (t == w.best_t && rf.rank > w.best_rank))) {
+            w.best_t = t;
+            w.best_rank = rf.rank;
+            w.best_prim = (int32_t)rf.prim;
+            w.best_inst = rf.inst;
+            ts.t_best = (float)t * (1.0f + 0x1p-20f);
+        }
+        ts.leaf = more ? ts.leaf - 7 : WBVH_NO_LEAF;  // ~((first + 1) << 3 | (more - 1)) = ~v - 7
+    }
+    if (ts.node >= 0) wbvh4c_visit<R>(ts, sc, stk);
+    if (ts.leaf == WBVH_NO_LEAF && ts.node < 0 && ts.node != WBVH_DONE) {
+        ts.leaf = ts.node;
+        ts.node = wbvh4c_pop(ts, stk);
+    }
+}
+template <typename R, int MAXD, class STK>
+__device__ __forceinline__ bool xwalk_finish(const XWalkU<R>& w, const DSceneView<R>&, const Ray<R>&,
+                                             HitMin<R, MAXD>& hm, STK&) {
+    hm.t = w.best_t;
+    hm.prim = (uint32_t)w.best_prim;
+    hm.depth = w.best_inst >= 0 ? 1 : 0;
+    hm.inst[0] = (uint32_t)w.best_inst;
+    return w.best_prim >= 0;
+}
+// (the prefiltered walk's trip takes the world ray for the same call)
+template <typename R, class STK>
+__device__ __forceinline__ void xwalk_trip(XWalk& w, const DSceneView<R>& sc, STK& stk, const Ray<R>&) {
+    xwalk_trip<R>(w, sc, stk);
+}
+
 // Small plane-only scenes (at most EXACT_SLOTS_MAX slots, EXACT_SIG_SLOTS_PF): the prefilter over
 // every slot of the culling tree in slot order instead of the walk: the slot index is wave-
 // uniform, so each f32 record arrives by scalar load and no lane waits for another's walk (no
@@ -3212,7 +3285,9 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             // ballot shows p.wave_wait lanes (default XWALK_WAIT) done, then those lanes run the
             // candidate tests, shade and begin their next segment, as the f32 world-BVH loop above.
             static_assert(EXACT && sizeof(R) == 8 && SIG::lstack, "persistent exact walk: f64, LDS stack");
-            XWalk xw;
+            // the prefiltered walk (plane-only scenes) or the unfiltered one (EXACT_SIG_WORLD: spheres)
+            using XW = typename TypeIf<SIG::exact == EXACT_SIG_WORLD, XWalkU<R>, XWalk>::type;
+            XW xw;
             xw.ts.node = WBVH_DONE;
             xw.ts.leaf = WBVH_NO_LEAF;
             bool active = false;
@@ -3231,7 +3306,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                     const bool going = active && xw.busy();
                     const uint64_t gm = __ballot(going);
                     if (gm == 0ull || (uint32_t)__popcll(am & ~gm) >= wait_min) break;
-                    if (going) xwalk_trip<R>(xw, sc, stack);
+                    if (going) xwalk_trip<R>(xw, sc, stack, ray);
                 }
                 const unsigned long long t1 = stamp();
                 if (active && !xw.busy()) {

@@ -157,6 +157,15 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
             vw.n_nodes = 0;  // (the world walk never reads the reference node array)
             const uint32_t scene = lds_scene_bytes(vw, MAXD);
             const uint32_t stk = (vw.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(uint16_t);
+            const char* pe = std::getenv("NRT_EXACT_PERSIST");
+            if (!(pe && pe[0] == '0')) {  // the walk kept across shading rounds (XWalkU)
+                using XWP = dev::ExactSig<dev::EXACT_SIG_WORLD, WBVH_COMPACT, true, true>;
+                RenderParams q = p;
+                if (!q.wave_wait) q.wave_wait = 56u;
+                if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, 0, XWP>(q, vw, ring + stk + scene, stream);
+                else launch_variant<R, G, MAXD, EXACT, false, 0, XWP>(q, vw, ring + stk, stream);
+                return;
+            }
             if (scene <= LDS_SCENE_LIMIT) launch_variant<R, G, MAXD, EXACT, true, 0, XW>(p, vw, ring + stk + scene, stream);
             else launch_variant<R, G, MAXD, EXACT, false, 0, XW>(p, vw, ring + stk, stream);
             return;
