@@ -16,6 +16,8 @@ run c4_f32_chacha --scene scenes/utah-teapot-scene.json --rng chacha8 --steps 8 
 run c4_f64 --scene scenes/utah-teapot-scene.json --precision f64 --rng chacha8 --steps 4 && \
 run c1_f32 --scene scenes/spheres.toml --width 400 --height 225 --spp 16 && \
 run c1_f32_big --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 && \
+run c1_f64 --scene scenes/spheres.toml --width 400 --height 225 --spp 16 --precision f64 --rng chacha8 --steps 8 && \
+run c1_f64_big --scene scenes/spheres.toml --width 1920 --height 1080 --spp 64 --precision f64 --rng chacha8 --steps 4 && \
 run c5_f32 && \
 run c5_f32_chacha --rng chacha8 --steps 8 && \
 run c5_f64_chacha --precision f64 --rng chacha8 --steps 4 && \
