@@ -285,7 +285,8 @@ int nrt_image_load(const char* path, uint32_t* width, uint32_t* height, float* r
 int nrt_image_to_rgb8(const float* rgb, size_t n_floats, float gamma, uint8_t* out);
 
 /* Tests: first `count` next_u64 draws of `lanes` consecutive pixel streams
- * (rng 0 ChaCha8: stream = pixel index; rng 1 Philox4x32-10: counter (pixel, sample, pair)),
+ * (rng 0 ChaCha8: stream = pixel index, below 2^32 as every image pixel's: stream0 + lanes > 2^32 - 1
+ * is NRT_E_INVALID; rng 1 Philox4x32-10: counter (pixel, sample, pair)),
  * or with rng 2 the f32 render loop's Philox2x32-10 blocks: word k of lane l = the block
  * of (pixel stream0 + l, sample, step k), lo | hi << 32 (count <= 256, sample < 2^24). */
 int nrt_debug_rng(uint32_t rng, uint64_t stream0, uint32_t lanes, uint32_t count, uint32_t sample, uint64_t* out);
