@@ -171,9 +171,12 @@ def test_philox_wave_size_is_bitwise_identical(monkeypatch, scene, precision, tr
         np.testing.assert_array_equal(s.render(precision=precision, rng="philox", trace=trace), full)
 
 
-def test_row_interleave_is_bitwise_identical():
+@pytest.mark.parametrize("scene", ["scenes/cornell-box-scene.json",
+                                   "scenes/utah-teapot-scene.json",  # the persistent prefiltered walk, large tree
+                                   "scenes/spheres.toml"])           # the persistent unfiltered walk (XWalkU)
+def test_row_interleave_is_bitwise_identical(scene):
     # RNG keyed by pixel index: any row partition gives the same pixels
-    scene, w, h, spp = "scenes/cornell-box-scene.json", 32, 21, 4
+    w, h, spp = 32, 21, 4
     s = load(scene, w, h, spp)
     full = s.render(precision="f64", rng="chacha8")
     for stride in (2, 3, 8):
