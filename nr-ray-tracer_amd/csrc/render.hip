@@ -261,8 +261,9 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
     DeviceGuard guard(ds->device);  // memset, occupancy query and launch on the scene's device
     hipStream_t stream = (hipStream_t)stream_ptr;
     RenderParams q = p;
-    if (q.wave_wait == 0 && precision != 0)  // if-if trips (KF_FLAT world BVH) shade at 24 finished lanes (C4 34.6 -> 34.3 ms),
-        q.wave_wait = ds->flat ? 24u : 32u;  // the sphere / texture variant at 32 (spheres.toml 1080p: 31.06 ms at 24, 30.71 at 32)
+    if (q.wave_wait == 0 && precision != 0)  // if-if trips (KF_FLAT world BVH) shade at 24 finished lanes (C4 34.6 -> 34.3 ms;
+        q.wave_wait = ds->flat ? 24u : 48u;  // 32 / 40: 31.2 / 31.3 against 30.9 ms, round 5), the sphere / texture variant at 48
+                                             // (spheres.toml 1080p: 27.64 / 27.26 / 26.84 / 26.83 / 33.24 ms at 32 / 40 / 48 / 56 / 64)
                                              // (the exact kernel's persistent walk: its own default, launch_impl.hpp)
     // Persistent lanes: claims of 128/spp pixels (1..8).  Short pixels end often, and a claim per
     // finished pixel stalls the wave on the atomic's return (earth f64 spp 16: 6.26 -> 5.87 ms at
