@@ -58,10 +58,15 @@ static uint64_t resident_blocks(K kernel, uint32_t lds_bytes) {
 // smallest power of two with >= 1024 samples per group (a group must outlast the
 // longest path in flight for the ring of two to keep lanes busy; small groups keep
 // a wave's rays on few pixels), halved while the launch has fewer than two groups
-// per resident wave (or fewer than 16 while groups keep > 512 samples).
+// per resident wave (or fewer than NRT_GROUPS_PER_WAVE while groups keep > 512 samples).
 // `resident(lds)` = blocks the device keeps resident with `lds` bytes of dynamic LDS,
 // `launch(blocks, lds, params)` enqueues the kernel (a static instantiation or a
 // scene-specialised module function, jit.hip).
+#ifndef NRT_GROUPS_PER_WAVE
+#define NRT_GROUPS_PER_WAVE 4  // (16 before frames were pipelined: with the next launch filling the SIMDs a
+                               // launch's last groups leave idle, larger groups win: row shards of C5 at
+                               // N = 4 / 8 2.588 -> 2.566 / 1.336 -> 1.333 ms, full frames unchanged)
+#endif
 template <int MAXD, class Resident, class Launch>
 static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&& resident, Launch&& launch) {
     const uint32_t npix = p0.pixel_end - p0.pixel_begin;
@@ -73,11 +78,16 @@ static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&&
         while (wp < 64 && (uint64_t)wp * p.spp < 1024) wp <<= 1;
         const uint64_t w0 = resident(lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
         // halve while the launch has fewer than two groups per resident wave, or
-        // (down to 512 samples per group) fewer than 16: the last groups to finish
-        // set the tail, which matters for the short launches of a row shard
-        // (C5 at N = 8: 4.6 -> 9.1 groups per wave, -5 % kernel time)
+        // (down to 512 samples per group) fewer than NRT_GROUPS_PER_WAVE: the last groups to
+        // finish set the tail of a lone launch (C5 at N = 8 without pipelining: 4.6 -> 9.1
+        // groups per wave, -5 % kernel time, round 3); pipelined launches overlap that tail
         auto groups = [&](uint32_t w) { return (uint64_t)(npix + w - 1) / w; };
-        while (wp > 1 && (groups(wp) < 2 * w0 || ((uint64_t)wp * p.spp > 512 && groups(wp) < 16 * w0))) wp >>= 1;
+        uint64_t gpw = NRT_GROUPS_PER_WAVE;  // knob NRT_GROUPS_PER_WAVE (A/B runs)
+        if (const char* e = std::getenv("NRT_GROUPS_PER_WAVE")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v >= 1 && v <= 64) gpw = (uint64_t)v;
+        }
+        while (wp > 1 && (groups(wp) < 2 * w0 || ((uint64_t)wp * p.spp > 512 && groups(wp) < gpw * w0))) wp >>= 1;
     }
     const uint64_t waves_res = resident(lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
     p.wave_pixels = wp;

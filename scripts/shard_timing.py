@@ -34,7 +34,7 @@ NSTREAMS = int(os.environ.get("SHARD_STREAMS", "2"))  # pipelined mode: launches
 pbufs = [buf] + [torch.zeros_like(buf) for _ in range(NSTREAMS - 1)]
 pstreams = [stream] + [torch.cuda.Stream(device="cuda:0") for _ in range(NSTREAMS - 1)]
 res, resq, resp = {}, {}, {}
-K = 8
+K = int(os.environ.get("SHARD_K", "8"))  # launches per pipelined measurement (the last one's tail is not overlapped)
 ns = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1, 2, 4, 8]
 for n in ns:
     rows = (H + n - 1) // n
