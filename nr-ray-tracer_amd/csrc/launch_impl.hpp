@@ -74,8 +74,12 @@ static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&&
     auto ring_bytes = [](uint32_t wp) { return dev::philox_pool_bytes<MAXD>(wp); };
     uint32_t wp = p.wave_pixels;
     if (!wp) {
+        // world-BVH kernels (MAXD < 0) take at least 8 pixels per group: their ring of four slots turns
+        // over less often (the teapot at spp 256: 4 / 8 / 16 / 32 pixels 30.87 / 30.00 / 29.93 / 32.04 ms;
+        // the spheres at spp 64 keep 16: 32 measured 27.05 against 26.77 ms; world lists keep 1024 samples)
+        constexpr uint32_t min_px = MAXD < 0 ? 8u : 1u;
         wp = 1;
-        while (wp < 64 && (uint64_t)wp * p.spp < 1024) wp <<= 1;
+        while (wp < 64 && ((uint64_t)wp * p.spp < 1024 || wp < min_px)) wp <<= 1;
         const uint64_t w0 = resident(lds_fixed + ring_bytes(wp)) * (dev::BLOCK / 64);
         // halve while the launch has fewer than two groups per resident wave, or
         // (down to 512 samples per group) fewer than NRT_GROUPS_PER_WAVE: the last groups to
