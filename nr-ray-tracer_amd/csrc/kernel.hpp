@@ -2750,6 +2750,10 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 #ifndef NRT_GRAB
 #define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
 #endif
+#ifndef NRT_GRAB_FLAT
+#define NRT_GRAB_FLAT 2  // ... for the solid-colour (KF_FLAT) kernels: C5 9.91 -> 9.86 ms, C4 29.82 -> 29.64 ms
+                         // (4 alternating runs; the textured earth: 5.14 -> 5.27 ms with 2, so it keeps 1)
+#endif
 #ifndef NRT_PROBE_HEAD
 // 1: skip queue heads an agent-scope load shows empty before the atomic (saved C5 ~2 MB of HBM
 // writes, but the extra round trip before each fetch cost C3 earth 6.67 -> 7.32 ms): off
@@ -3397,6 +3401,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // with two slots one long path of the previous group starves the wave's lanes
         // (world BVH: long and short paths mix), so the BVH modes keep four.
         constexpr uint32_t NS = philox_slots<MAXD>();
+        constexpr uint32_t GRAB = FLAT ? (uint32_t)NRT_GRAB_FLAT : (uint32_t)NRT_GRAB;  // groups per queue atomic
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
         const uint32_t GS = P * p.spp;  // samples per group (host: < 2^32)
@@ -3419,7 +3424,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // image region: node, texel and framebuffer lines shared in the XCD's L1s and L2), and no
         // head is contended by more than one XCD's waves until the tail.  A device-scope atomic
         // executes at the memory side (one ~32-B HBM write each; with one per group they were
-        // 45 % of the C5 launch's HBM writes): a wave takes NRT_GRAB consecutive groups per atomic
+        // 45 % of the C5 launch's HBM writes): a wave takes GRAB consecutive groups per atomic
         // (more per grab spreads the XCD's waves over a larger image region: guided runs of up
         // to 25 groups cost C4 +50 %, C5 +12 %), and skips heads an agent-scope load already
         // shows empty (a stale value only lags).  The XCD id only places work: never correctness.
@@ -3429,7 +3434,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t lcur = 0, lend = 0;  // groups of the last grab not yet taken (wave-uniform)
         auto fetch = [&](uint32_t r) {              // uniform: take the next group into (free) slot r
             uint32_t gid = 0xFFFFFFFFu;
-            if (NRT_GRAB > 1 && lcur < lend) {
+            if (GRAB > 1 && lcur < lend) {
                 gid = lcur++;
             } else {
                 if (lane == 0) {
@@ -3441,7 +3446,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         if (n == 0 || (NRT_PROBE_HEAD && __hip_atomic_load(head, __ATOMIC_RELAXED,
                                                                             __HIP_MEMORY_SCOPE_AGENT) >= n))
                             continue;
-                        const uint32_t k = qk ? 1u : (uint32_t)NRT_GRAB;  // a steal takes one group
+                        const uint32_t k = qk ? 1u : GRAB;  // a steal takes one group
                         const uint32_t t = atomicAdd(head, k);
                         if (t < n) {
                             gid = lo + t;
@@ -3453,7 +3458,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 }
                 gid = __builtin_amdgcn_readlane(gid, 0);
                 qk = __builtin_amdgcn_readlane(qk, 0);
-                if (NRT_GRAB > 1) {
+                if (GRAB > 1) {
                     lcur = __builtin_amdgcn_readlane(lcur, 0);
                     lend = __builtin_amdgcn_readlane(lend, 0);
                 }
