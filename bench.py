@@ -426,33 +426,28 @@ def run_library(args):
     for d in range(N):
         scene.upload(d)
     t_upload = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    # the library runs GPU 0's gathers and the un-permute on this stream, and the frame's host copy follows
+    # them here too: GPU 0 then runs this stream + the library's three render streams, the process's 4
+    # hardware queues (GPU_MAX_HW_QUEUES; a fifth stream would share a queue with a render)
     stream = torch.cuda.current_stream()
+    scene.prepare(precision=args.precision, rng=args.rng, device=0, trace=args.trace, gpus=N)  # RCCL comms, buffers
     NB = max(2, args.pipeline or 2)  # device / pinned host frames (the library keeps its own buffer sets)
     frames = [torch.empty((H, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
     host = [torch.empty((H, W, 3), dtype=torch.float32).pin_memory() for _ in range(NB)]
-    copy_stream = torch.cuda.Stream(device=dev)
-    copied = [None] * NB
     cev = []
-    with torch.cuda.stream(copy_stream):  # (its hardware queue is created at its first launch)
-        torch.zeros(1, device=dev)
     torch.cuda.synchronize()
+    t_prepare = time.perf_counter() - t0
 
     def step(k, timed):
-        slot = k % NB
-        if copied[slot] is not None:
-            stream.wait_event(copied[slot])  # frame `slot` was copied out NB frames ago
+        slot = k % NB  # (frames[slot] and host[slot] were last used NB frames ago, earlier on this stream)
         scene.render_device(frames[slot].data_ptr(), H * W * 3, precision=args.precision, rng=args.rng, device=0,
                             stream=stream.cuda_stream, trace=args.trace, gpus=N)
         if not args.kernel_only:
-            ready = torch.cuda.Event()
-            ready.record(stream)
-            copy_stream.wait_event(ready)
             c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(copy_stream):
-                c0.record(copy_stream)
-                host[slot].view(-1).copy_(frames[slot].view(-1), non_blocking=True)
-                c1.record(copy_stream)
-            copied[slot] = c1
+            c0.record(stream)
+            host[slot].view(-1).copy_(frames[slot].view(-1), non_blocking=True)
+            c1.record(stream)
             if timed:
                 cev.append((c0, c1))
 
@@ -482,7 +477,8 @@ def run_library(args):
     kern_ms = tm["period_ms"] if tm["period_ms"] > 0 else tm["kernel_ms"][0]
     report(args, nrt, scene, n_gpus=N, rows=rows, elapsed=elapsed, kern_ms=kern_ms, d2h_ms=d2h_ms,
            timings_s={"runtime_init": round(t_init, 4), "scene_load_and_bvh": round(t_load, 4),
-                      "upload": round(t_upload, 4), "jit_compile": jit_after["compile_s"],
+                      "upload": round(t_upload, 4), "multi_gpu_prepare": round(t_prepare, 4),
+                      "jit_compile": jit_after["compile_s"],
                       "first_frame": None if first_frame is None else round(first_frame, 4)},
            frame_sha=frame_sha, jit_before=jit_before, jit_after=jit_after,
            kernel_variant=kernel_variant_of(jit_before, jit_after, args.steps * N),
@@ -498,6 +494,10 @@ def run_library(args):
 
 def main():
     args = parse_args()
+    if os.environ.get("NRT_MULTI_LOOPBACK", "0") not in ("", "0") and not os.environ.get("NRT_BENCH_DIAG_LOOPBACK"):
+        # the library's test-only loopback (every shard of a gpus = N render on GPU 0, the gather as
+        # device copies) would time N shards on one GPU as an N-GPU line: never a measurement
+        raise SystemExit("bench.py: NRT_MULTI_LOOPBACK is set (test-only multi-GPU loopback); unset it to measure")
     if args.cpu_only:
         cpu = cpu_baseline(args)
         print(json.dumps({"metric": "Msamples/sec (CPU baseline, oracle)", "value": cpu["value"], "unit": "Msamples/s",

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define NRT_ABI_VERSION 6
+#define NRT_ABI_VERSION 7
 
 enum {
     NRT_OK = 0,
@@ -121,8 +121,8 @@ typedef struct {
     /* 0: one device (`device`), the rows above.  N >= 1: the whole frame over the N devices
      * device .. device+N-1 of this process (Camera::render's one call over the whole machine,
      * lib/camera.rs:315-316): device first+r renders rows y = r (mod N) into its HBM,
-     * one RCCL ncclGather (librccl, dlopen'ed) brings the shards to the first device, which
-     * un-permutes them into the frame.  Needs row_offset 0 and row_stride <= 1; the frame is the
+     * one RCCL ncclGather (librccl, dlopen'ed; N = 1: a device copy, nothing to exchange) brings the
+     * shards to the first device, which un-permutes them into the frame.  Needs row_offset 0 and row_stride <= 1; the frame is the
      * same bits as gpus = 0 (pixels and their RNG streams do not depend on the device).  The
      * scene owns the communicators and shard buffers (created on first use, freed with it). */
     uint32_t gpus;
@@ -254,10 +254,18 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
  * asynchronous: returns after enqueueing. */
 int nrt_render_device(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts,
                       float* dev_out_rgb, size_t out_len, void* hip_stream);
-/* With opts->gpus = N >= 1: dev_out_rgb (W*H*3 f32) and hip_stream belong to the first device;
- * every device's render and the gather are enqueued and the call returns; hip_stream waits for
- * the frame, which is written only after hip_stream's prior work.  Consecutive calls pipeline:
- * frame k+1's renders may start while frame k's last paths, gather and un-permute run. */
+/* With opts->gpus = N >= 1: dev_out_rgb (W*H*3 f32) and hip_stream belong to the first device
+ * (a stream of another device: NRT_E_INVALID); every device's render and the gather are enqueued
+ * and the call returns.  The first device's gather and the un-permute run on hip_stream itself,
+ * after its prior work, so the library adds only its render streams to the caller's.  Consecutive
+ * calls pipeline: frame k+1's renders may start while frame k's last paths, gather and un-permute
+ * run. */
+/* Everything a render of (scene, camera, opts) needs before its first launch, done now (ABI 7): the
+ * upload to the device, and with opts->gpus = N the upload to every device, the RCCL communicators
+ * and the shard / staging buffers, so a timed first render (render.rs:57-62) pays none of it.
+ * NRT_E_UNSUPPORTED when gpus >= 2 and librccl (ncclGather, ncclCommInitAll) is not usable: a host
+ * may then render row shards per device itself (nrt_render_opts row_offset / row_stride). */
+int nrt_render_prepare(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts);
 /* HIP-event times (ms) of the scene's last gpus >= 1 render (waits for it): out[d] = the render
  * launch on device first+d, d < N (begin to end; consecutive frames overlap, so this can include the
  * previous frame's tail); out[N] = the gather + un-permute on the first device (from its own render's

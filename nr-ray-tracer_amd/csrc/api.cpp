@@ -9,6 +9,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "flatten.hpp"
@@ -24,8 +25,8 @@ struct nrt_scene {
     FlatScene flat;
     std::mutex mu;
     std::vector<DeviceScene*> per_device;  // index = HIP ordinal
-    // multi-GPU renders (nrt_render_opts.gpus): one context per (first device, N), the last used
-    std::map<std::pair<int, int>, MultiRender*> multi;
+    // multi-GPU renders (nrt_render_opts.gpus): one context per (first device, N, loopback), the last used
+    std::map<std::tuple<int, int, bool>, MultiRender*> multi;
     MultiRender* last_multi = nullptr;
     ~nrt_scene() {
         for (auto& kv : multi) gpu_multi_free(kv.second);  // (before the device scenes they render)
@@ -65,6 +66,8 @@ int guarded(int fail_code, F&& f) {
         return set_error(NRT_E_DEVICE, "out of memory");
     } catch (const std::invalid_argument& e) {  // a bad argument, whichever call found it
         return set_error(NRT_E_INVALID, e.what());
+    } catch (const UnsupportedError& e) {
+        return set_error(NRT_E_UNSUPPORTED, e.what());
     } catch (const std::exception& e) {
         std::string m = e.what();
         if (m.find("outside the accelerated path") != std::string::npos) return set_error(NRT_E_UNSUPPORTED, m);
@@ -346,20 +349,43 @@ void check_opts(const nrt_render_opts* o) {
         throw std::invalid_argument("gpus >= 1 renders the whole frame: row_offset must be 0 and row_stride <= 1");
 }
 
+// NRT_MULTI_LOOPBACK=1 (tests only): a gpus = N render runs its N row shards on the first device,
+// the gather as device-to-device copies (multi.hip), so the N-GPU code runs on a one-GPU box
+bool multi_loopback() {
+    const char* e = std::getenv("NRT_MULTI_LOOPBACK");
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+
 // The multi-GPU context of opts (gpus >= 1): devices first .. first + gpus - 1, each with the
-// scene uploaded, one RCCL communicator each (multi.hip).
+// scene uploaded, one RCCL communicator each (multi.hip).  The context (communicators: seconds) is
+// built outside the scene's lock, so other renders of the scene do not wait for it.
 MultiRender* multi_render(nrt_scene* s, const nrt_render_opts* o) {
     const int n = gpu_device_count();
     if (n <= 0) throw std::runtime_error("HIP error in device query: no GPU device available");
     const int first = o->device < 0 ? 0 : o->device;
-    if ((int64_t)first + (int64_t)o->gpus > (int64_t)n)
+    const bool loop = multi_loopback();
+    if (loop ? first >= n : (int64_t)first + (int64_t)o->gpus > (int64_t)n)
         throw std::invalid_argument("gpus = " + std::to_string(o->gpus) + " from device " + std::to_string(first) +
                                     ": only " + std::to_string(n) + " device(s) visible");
+    const auto key = std::make_tuple(first, (int)o->gpus, loop);
+    {
+        std::lock_guard<std::mutex> lock(s->mu);
+        auto it = s->multi.find(key);
+        if (it != s->multi.end()) {
+            s->last_multi = it->second;
+            return it->second;
+        }
+    }
     std::vector<DeviceScene*> scenes;
-    for (uint32_t d = 0; d < o->gpus; ++d) scenes.push_back(device_scene(s, first + (int)d));
+    for (uint32_t d = 0; d < o->gpus; ++d) scenes.push_back(device_scene(s, loop ? first : first + (int)d));
+    MultiRender* made = gpu_multi_create(scenes, loop);
     std::lock_guard<std::mutex> lock(s->mu);
-    MultiRender*& m = s->multi[std::make_pair(first, (int)o->gpus)];
-    if (!m) m = gpu_multi_create(scenes);
+    MultiRender*& m = s->multi[key];
+    if (m) {  // another thread built it meanwhile: keep theirs
+        gpu_multi_free(made);
+    } else {
+        m = made;
+    }
     s->last_multi = m;
     return m;
 }
@@ -656,6 +682,24 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
             throw;
         }
         device_free(d, dev);
+        return NRT_OK;
+    });
+}
+
+int nrt_render_prepare(const nrt_scene* scene, const nrt_camera* camera, const nrt_render_opts* opts) {
+    return guarded(NRT_E_DEVICE, [&]() {
+        if (!scene || !camera) throw std::invalid_argument("null argument");
+        check_opts(opts);
+        nrt_scene* s = const_cast<nrt_scene*>(scene);
+        if (!opts || !opts->gpus) {
+            device_scene(s, resolve_device(opts));
+            return NRT_OK;
+        }
+        std::string why;
+        if (opts->gpus > 1 && !multi_loopback() && !gpu_multi_rccl_usable(&why))
+            throw UnsupportedError("gpus >= 1 needs RCCL's ncclGather: " + why);
+        MultiRender* m = multi_render(s, opts);
+        gpu_multi_prepare(m, (uint32_t)camera->width, (uint32_t)camera->height);
         return NRT_OK;
     });
 }

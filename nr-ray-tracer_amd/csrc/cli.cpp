@@ -21,6 +21,7 @@
 #include <cstring>
 #include <regex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nrt.h"
@@ -315,20 +316,58 @@ int main(int argc, char** argv) {
     const uint32_t W = (uint32_t)cam.width, H = (uint32_t)cam.height;
     std::vector<float> img((size_t)W * H * 3);
 
-    // GPU runtime start and the scene's upload before the timed render (render.rs:57-62 times
-    // scene.render alone; the scene was built before it), reported apart with -v
+    // GPU runtime start, the scene's upload and (--gpus N > 1) the multi-GPU context before the timed
+    // render (render.rs:57-62 times scene.render alone; the scene was built before it), reported apart
+    // with -v
     const auto ti = std::chrono::steady_clock::now();
     int ndev = nrt_device_count();
     if (gpus < 1) gpus = 1;
     if (gpus > ndev) die("requested " + std::to_string(gpus) + " GPUs, " + std::to_string(ndev) + " visible");
-    for (int g = 0; g < gpus; ++g)
-        if (nrt_scene_upload(sc, g) != NRT_OK) die(nrt_last_error());
+    // --gpus N > 1: the library's multi-GPU render (nrt_render_opts.gpus): rows interleaved over
+    // devices 0 .. N-1, one RCCL gather to device 0, un-permuted there; without a usable
+    // librccl (nrt_render_prepare: NRT_E_UNSUPPORTED) one host thread per device renders its row shard
+    // and the frame is un-permuted here
+    bool shards = false;
+    if (gpus > 1) {
+        opts.gpus = (uint32_t)gpus;
+        const int rc = nrt_render_prepare(sc, &cam, &opts);
+        if (rc == NRT_E_UNSUPPORTED) {
+            if (verbose) fprintf(stderr, " multi-GPU render without RCCL (%s): per-device row shards\n", nrt_last_error());
+            opts.gpus = 0;
+            shards = true;
+            for (int g = 0; g < gpus; ++g)
+                if (nrt_scene_upload(sc, g) != NRT_OK) die(nrt_last_error());
+        } else if (rc != NRT_OK) {
+            die(nrt_last_error());
+        }
+    } else if (nrt_render_prepare(sc, &cam, &opts) != NRT_OK) {
+        die(nrt_last_error());
+    }
     const double init_secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - ti).count();
     const auto t0 = std::chrono::steady_clock::now();
-    // --gpus N > 1: the library's multi-GPU render (nrt_render_opts.gpus): rows interleaved over
-    // devices 0 .. N-1, one RCCL gather to device 0, un-permuted there
-    if (gpus > 1) opts.gpus = (uint32_t)gpus;
-    if (nrt_render(sc, &cam, &opts, img.data(), img.size(), nullptr, nullptr) != NRT_OK) die(nrt_last_error());
+    if (shards) {
+        std::vector<std::vector<float>> part((size_t)gpus);
+        std::vector<std::string> err((size_t)gpus);
+        std::vector<std::thread> th;
+        for (int g = 0; g < gpus; ++g)
+            th.emplace_back([&, g]() {
+                nrt_render_opts o = opts;
+                o.device = g;
+                o.row_offset = (uint32_t)g;
+                o.row_stride = (uint32_t)gpus;
+                part[(size_t)g].resize((size_t)nrt_rows_selected(H, &o) * W * 3);
+                if (nrt_render(sc, &cam, &o, part[(size_t)g].data(), part[(size_t)g].size(), nullptr, nullptr) != NRT_OK)
+                    err[(size_t)g] = nrt_last_error();
+            });
+        for (auto& t : th) t.join();
+        for (const auto& e : err)
+            if (!e.empty()) die(e);
+        for (uint32_t y = 0; y < H; ++y)  // frame row y = shard y % N, its row y / N
+            memcpy(&img[(size_t)y * W * 3], &part[y % (uint32_t)gpus][(size_t)(y / (uint32_t)gpus) * W * 3],
+                   (size_t)W * 3 * sizeof(float));
+    } else if (nrt_render(sc, &cam, &opts, img.data(), img.size(), nullptr, nullptr) != NRT_OK) {
+        die(nrt_last_error());
+    }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (verbose) {
         const double samples = (double)W * H * (double)cam.samples_per_pixel;

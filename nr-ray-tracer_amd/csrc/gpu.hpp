@@ -16,8 +16,11 @@ struct MultiRender;
 
 // Multi-GPU render in one process (multi.hip): scenes[d] on device first + d (consecutive), one
 // RCCL communicator per device (ncclCommInitAll), rows y = d (mod N) on device d, one ncclGather
-// to the first device and a row un-permute there.  p is the full-frame RenderParams.
-MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes);  // throws (no librccl, HIP/RCCL errors)
+// to the first device and a row un-permute there.  p is the full-frame RenderParams.  loopback
+// (tests): every scenes[d] is on the first device and the gather is device-to-device copies.
+MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes, bool loopback);  // throws
+bool gpu_multi_rccl_usable(std::string* why);
+void gpu_multi_prepare(MultiRender* m, uint32_t width, uint32_t height);  // shard / staging buffers now  // librccl loadable with ncclGather / ncclCommInitAll
 void gpu_multi_free(MultiRender* m);
 int gpu_multi_first(const MultiRender* m);
 int gpu_multi_count(const MultiRender* m);

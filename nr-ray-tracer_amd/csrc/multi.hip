@@ -5,17 +5,32 @@
 // whole machine (rayon's global pool, lib/camera.rs:315-316); this is that call for a node of
 // MI355Xs.  nrt_render / nrt_render_device with nrt_render_opts.gpus = N reach it.
 //
-// Layout per context (one per (first device, N) of a scene), PIPE buffer sets so frame k+1's
-// renders can start while frame k's gather and un-permute run (and while frame k's slowest
+// Layout per context (one per (first device, N, loopback) of a scene), PIPE (4) buffer sets so frame
+// k+1's renders can start while frame k's gather and un-permute run (and while frame k's slowest
 // paths finish: the render streams of a device overlap one frame's tail with the next frame's
-// start).  Two sets: three in flight measured N = 8 shards 0.931 -> 0.935-0.940 of linear but the
-// whole C5 step 1-2 % slower (more streams than the process's 4 hardware queues: the host copy then
-// shares a queue with a render):
-//   device d:  rows[PIPE]   (rows_max x W x 3 f32 each), render streams rs[PIPE], one comm stream cs
-//   device 0:  staging[PIPE] (N x rows_max x W x 3 f32), the gather's receive buffers
-// The comm stream carries every gather of its device in issue order (RCCL requires the same
-// order on every rank; one stream per communicator keeps it), after an event of the frame's
-// render stream.  One host thread enqueues all devices: every call here is asynchronous.
+// start):
+//   device d:  rows[PIPE]   (rows_max x W x 3 f32 each), render streams rs[STREAMS]; d >= 1 one comm
+//              stream cs that carries every gather of its device in issue order (RCCL requires the
+//              same order on every rank; one stream per communicator keeps it)
+//   device 0:  staging[PIPE] (N x rows_max x W x 3 f32), the gather's receive buffers.  Its gathers
+//              and the un-permute run on the CALLER's stream (nrt_render_device's hip_stream; the
+//              context's host stream for nrt_render), chained to the previous frame's gather when
+//              the caller switches streams, so device 0 runs the caller's stream + STREAMS (3)
+//              render streams: a caller that copies the frame out on that same stream stays within
+//              the process's 4 hardware queues (GPU_MAX_HW_QUEUES).
+// One host thread enqueues all devices: every call here is asynchronous.
+//
+// N = 1 has nothing to exchange: its "gather" is a device-to-device copy into the staging buffer
+// and no communicator is made.  (Measured on C5 through a communicator of one: ncclGather's kernel
+// cost 0.12-0.3 ms of device time per 9.9-ms frame, 1.2-3 % -- more with fewer channels -- against
+// 0.015 ms for the copy and the un-permute: the persistent render grid fills every CU, and the RCCL
+// kernel's workgroups, 20 KB of LDS each, wait at the head of their queue for a render's tail.)
+//
+// Loopback (test only, NRT_MULTI_LOOPBACK=1 at context creation, api.cpp): the N logical shards all
+// live on the first device, each with its own buffers and streams, and each shard's ncclGather is a
+// device-to-device copy into the same staging slot on the same comm stream; everything else (row
+// counts, short last shards, buffer-set rotation, event chaining, the un-permute) is the code the
+// N-GPU render runs, so a one-GPU box exercises it.  bench.py refuses the mode.
 //
 // librccl is resolved with dlopen (soname librccl.so.1: the copy torch already loaded when it
 // is in the process, else /opt/rocm's), so libnrt.so loads and renders on one device without it.
@@ -26,6 +41,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -114,17 +130,38 @@ __global__ void __launch_bounds__(256) unpermute_rows(const float* __restrict__ 
     }
 }
 
-constexpr int PIPE = 2;  // buffer sets (frames in flight)
+// Render streams per device (frames rotate over them): 3, so device 0 runs the caller's stream + 3
+// render streams = the process's 4 hardware queues when the caller copies the frame out on the same
+// stream it passes (bench.py).  Buffer sets: one more than the streams.  The render kernel is
+// persistent (its grid is the resident capacity), so the gather's kernel of frame k finds CU slots only
+// when a later render's workgroups leave, at that render's tail; with sets = streams, frame k + 3's
+// render waited for that gather, and a frame's tail went unfilled (C5 at N = 1 through RCCL: -1.2 %);
+// with a spare set it waits for frame k - 1's gather, long done.  NRT_MULTI_STREAMS (1-3) and
+// NRT_MULTI_PIPE (sets, >= streams, <= 4) at context creation for A/B runs.
+constexpr int STREAMS = 3;
+constexpr int PIPE = 4;  // (array capacity; sets in use default to the streams, NRT_MULTI_PIPE)
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = std::getenv(name);
+    const long v = e ? std::strtol(e, nullptr, 10) : dflt;
+    return v >= lo && v <= hi ? (int)v : dflt;
+}
+
+// RCCL's first init prints a banner on stdout; the redirect around it swaps the process-wide fd 1,
+// so two contexts created at once must not interleave it (one lock for every context)
+std::mutex g_stdout_mu;
 
 }  // namespace
 
 struct MultiRender {
     int first = 0, n = 0;
-    std::vector<DeviceScene*> scenes;  // scenes[d] lives on device first + d
+    bool loopback = false;             // N logical shards on device `first` (test only)
+    int pipe = PIPE;                   // buffer sets in use (<= PIPE)
+    int nrs = STREAMS;                 // render streams per device in use (<= STREAMS, <= pipe)
+    std::vector<DeviceScene*> scenes;  // scenes[d] lives on device dev_of(d)
     std::vector<ncclComm_t> comms;
     struct Dev {
-        hipStream_t rs[PIPE] = {};  // render streams (frames rotate)
-        hipStream_t cs = nullptr;   // comm stream (every gather, in issue order)
+        hipStream_t rs[STREAMS] = {};  // render streams (frames rotate)
+        hipStream_t cs = nullptr;   // comm stream (every gather, in issue order); d = 0: the caller's
         float* rows[PIPE] = {};
         hipEvent_t rendered[PIPE] = {}, gathered[PIPE] = {};
         hipEvent_t t0[PIPE] = {}, t1[PIPE] = {};  // render kernel timing
@@ -132,8 +169,7 @@ struct MultiRender {
     std::vector<Dev> dev;
     float* staging[PIPE] = {};
     float* frame = nullptr;  // nrt_render's device frame on the first device
-    hipStream_t host_stream = nullptr;
-    hipEvent_t in_ev[PIPE] = {}, done_ev[PIPE] = {};
+    hipStream_t host_stream = nullptr;  // device 0's comm stream for nrt_render (the host copy follows)
     hipEvent_t g0[PIPE] = {}, g1[PIPE] = {};  // gather + un-permute timing
     // frame-period window (nrt_render_timings): w0 = the start of the first device's render of the
     // window's first frame, w_frames = frames enqueued in the window (consecutive frames' renders overlap,
@@ -145,20 +181,21 @@ struct MultiRender {
     uint64_t frames = 0;
     int last = -1;  // buffer set of the last frame
     std::mutex mu;
+    int dev_of(int d) const { return loopback ? first : first + d; }
 };
 
 namespace {
 
 void free_buffers(MultiRender* m) {
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
-        for (int s = 0; s < PIPE; ++s) {
-            if (m->dev[d].rows[s]) (void)hipFree(m->dev[d].rows[s]);
-            m->dev[d].rows[s] = nullptr;
+        Guard g(m->dev_of(d));
+        for (int s = 0; s < m->pipe; ++s) {
+            if (m->dev[(size_t)d].rows[s]) (void)hipFree(m->dev[(size_t)d].rows[s]);
+            m->dev[(size_t)d].rows[s] = nullptr;
         }
     }
     Guard g(m->first);
-    for (int s = 0; s < PIPE; ++s) {
+    for (int s = 0; s < m->pipe; ++s) {
         if (m->staging[s]) (void)hipFree(m->staging[s]);
         m->staging[s] = nullptr;
     }
@@ -167,12 +204,17 @@ void free_buffers(MultiRender* m) {
     m->W = m->H = m->rows_max = 0;
 }
 
+// every enqueued frame done: the render and comm streams, and (device 0's gathers ran on callers'
+// streams) the last gather event of every buffer set
 void sync_all(MultiRender* m) {
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
-        for (int s = 0; s < PIPE; ++s)
-            if (m->dev[d].rs[s]) (void)hipStreamSynchronize(m->dev[d].rs[s]);
-        if (m->dev[d].cs) (void)hipStreamSynchronize(m->dev[d].cs);
+        Guard g(m->dev_of(d));
+        const MultiRender::Dev& x = m->dev[(size_t)d];
+        for (int s = 0; s < m->nrs; ++s)
+            if (x.rs[s]) (void)hipStreamSynchronize(x.rs[s]);
+        for (int s = 0; s < m->pipe; ++s)
+            if (x.gathered[s]) (void)hipEventSynchronize(x.gathered[s]);
+        if (x.cs) (void)hipStreamSynchronize(x.cs);
     }
     if (m->host_stream) {
         Guard g(m->first);
@@ -187,14 +229,15 @@ void ensure_buffers(MultiRender* m, uint32_t W, uint32_t H) {
     const uint32_t rows_max = (H + (uint32_t)m->n - 1) / (uint32_t)m->n;
     const size_t shard = (size_t)rows_max * W * 3 * sizeof(float);
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
-        for (int s = 0; s < PIPE; ++s) {
-            hcheck(hipMalloc((void**)&m->dev[d].rows[s], shard), "hipMalloc(row shard)");
-            hcheck(hipMemset(m->dev[d].rows[s], 0, shard), "hipMemset(row shard)");  // rows past a short shard
+        Guard g(m->dev_of(d));
+        for (int s = 0; s < m->pipe; ++s) {
+            hcheck(hipMalloc((void**)&m->dev[(size_t)d].rows[s], shard), "hipMalloc(row shard)");
+            hcheck(hipMemset(m->dev[(size_t)d].rows[s], 0, shard), "hipMemset(row shard)");  // rows past a short shard
         }
+        hcheck(hipDeviceSynchronize(), "hipMemset(row shard)");  // (the render streams do not block on it)
     }
     Guard g(m->first);
-    for (int s = 0; s < PIPE; ++s) hcheck(hipMalloc((void**)&m->staging[s], shard * (size_t)m->n), "hipMalloc(staging)");
+    for (int s = 0; s < m->pipe; ++s) hcheck(hipMalloc((void**)&m->staging[s], shard * (size_t)m->n), "hipMalloc(staging)");
     m->W = W;
     m->H = H;
     m->rows_max = rows_max;
@@ -202,58 +245,66 @@ void ensure_buffers(MultiRender* m, uint32_t W, uint32_t H) {
 
 }  // namespace
 
-MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes) {
+MultiRender* gpu_multi_create(const std::vector<DeviceScene*>& scenes, bool loopback) {
     const Rccl& r = rccl();
-    if (!r.ok) throw std::runtime_error("HIP error in multi-GPU render: " + r.why);
+    const bool need_rccl = !loopback && scenes.size() > 1;
+    if (need_rccl && !r.ok) throw std::runtime_error("HIP error in multi-GPU render: " + r.why);
+    if (scenes.empty()) throw std::invalid_argument("multi-GPU render: no devices");
     auto* m = new MultiRender();
     m->n = (int)scenes.size();
+    m->loopback = loopback;
+    m->nrs = env_int("NRT_MULTI_STREAMS", STREAMS, 1, STREAMS);
+    m->pipe = env_int("NRT_MULTI_PIPE", m->nrs, m->nrs, PIPE);
     m->first = gpu_scene_device(scenes[0]);
     m->scenes = scenes;
     m->dev.resize(scenes.size());
     try {
         std::vector<int> devlist;
         for (int d = 0; d < m->n; ++d) {
-            if (gpu_scene_device(scenes[(size_t)d]) != m->first + d)
-                throw std::invalid_argument("multi-GPU render: devices must be consecutive ordinals");
-            devlist.push_back(m->first + d);
+            if (gpu_scene_device(scenes[(size_t)d]) != m->dev_of(d))
+                throw std::invalid_argument(loopback ? "multi-GPU loopback: every shard renders on the first device"
+                                                     : "multi-GPU render: devices must be consecutive ordinals");
+            devlist.push_back(m->dev_of(d));
         }
         for (int d = 0; d < m->n; ++d) {
-            Guard g(m->first + d);
+            Guard g(m->dev_of(d));
             MultiRender::Dev& x = m->dev[(size_t)d];
-            for (int s = 0; s < PIPE; ++s) {
+            for (int s = 0; s < m->nrs; ++s)
                 hcheck(hipStreamCreateWithFlags(&x.rs[s], hipStreamNonBlocking), "hipStreamCreate");
+            for (int s = 0; s < m->pipe; ++s) {
                 hcheck(hipEventCreateWithFlags(&x.rendered[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreateWithFlags(&x.gathered[s], hipEventDisableTiming), "hipEventCreate");
                 hcheck(hipEventCreate(&x.t0[s]), "hipEventCreate");
                 hcheck(hipEventCreate(&x.t1[s]), "hipEventCreate");
             }
-            hcheck(hipStreamCreateWithFlags(&x.cs, hipStreamNonBlocking), "hipStreamCreate");
+            if (d > 0) hcheck(hipStreamCreateWithFlags(&x.cs, hipStreamNonBlocking), "hipStreamCreate");
         }
         {
             Guard g(m->first);
             hcheck(hipStreamCreateWithFlags(&m->host_stream, hipStreamNonBlocking), "hipStreamCreate");
             hcheck(hipEventCreate(&m->w0), "hipEventCreate");
-            for (int s = 0; s < PIPE; ++s) {
-                hcheck(hipEventCreateWithFlags(&m->in_ev[s], hipEventDisableTiming), "hipEventCreate");
-                hcheck(hipEventCreateWithFlags(&m->done_ev[s], hipEventDisableTiming), "hipEventCreate");
+            for (int s = 0; s < m->pipe; ++s) {
                 hcheck(hipEventCreate(&m->g0[s]), "hipEventCreate");
                 hcheck(hipEventCreate(&m->g1[s]), "hipEventCreate");
             }
         }
-        m->comms.assign((size_t)m->n, nullptr);
-        // RCCL prints a version banner on stdout at its first init; a library keeps the caller's
-        // stdout clean (bench.py's one JSON line, a CLI writing an image to stdout): the banner goes
-        // to stderr
-        std::fflush(stdout);
-        const int saved = ::dup(1);
-        if (saved >= 0) (void)::dup2(2, 1);
-        const ncclResult_t ir = r.init_all(m->comms.data(), m->n, devlist.data());
-        std::fflush(stdout);
-        if (saved >= 0) {
-            (void)::dup2(saved, 1);
-            ::close(saved);
+        if (need_rccl) {
+            m->comms.assign((size_t)m->n, nullptr);
+            // RCCL prints a version banner on stdout at its first init; a library keeps the caller's
+            // stdout clean (bench.py's one JSON line, a CLI writing an image to stdout): the banner goes
+            // to stderr
+            std::lock_guard<std::mutex> lock(g_stdout_mu);
+            std::fflush(stdout);
+            const int saved = ::dup(1);
+            if (saved >= 0) (void)::dup2(2, 1);
+            const ncclResult_t ir = r.init_all(m->comms.data(), m->n, devlist.data());
+            std::fflush(stdout);
+            if (saved >= 0) {
+                (void)::dup2(saved, 1);
+                ::close(saved);
+            }
+            ncheck(ir, "ncclCommInitAll");
         }
-        ncheck(ir, "ncclCommInitAll");
     } catch (...) {
         gpu_multi_free(m);
         throw;
@@ -268,19 +319,20 @@ void gpu_multi_free(MultiRender* m) {
         if (c) (void)rccl().destroy(c);
     free_buffers(m);
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
+        Guard g(m->dev_of(d));
         MultiRender::Dev& x = m->dev[(size_t)d];
-        for (int s = 0; s < PIPE; ++s) {
+        for (int s = 0; s < m->pipe; ++s) {
             for (hipEvent_t e : {x.rendered[s], x.gathered[s], x.t0[s], x.t1[s]})
                 if (e) (void)hipEventDestroy(e);
-            if (x.rs[s]) (void)hipStreamDestroy(x.rs[s]);
         }
+        for (int s = 0; s < m->nrs; ++s)
+            if (x.rs[s]) (void)hipStreamDestroy(x.rs[s]);
         if (x.cs) (void)hipStreamDestroy(x.cs);
     }
     {
         Guard g(m->first);
-        for (int s = 0; s < PIPE; ++s)
-            for (hipEvent_t e : {m->in_ev[s], m->done_ev[s], m->g0[s], m->g1[s]})
+        for (int s = 0; s < m->pipe; ++s)
+            for (hipEvent_t e : {m->g0[s], m->g1[s]})
                 if (e) (void)hipEventDestroy(e);
         if (m->w0) (void)hipEventDestroy(m->w0);
         if (m->host_stream) (void)hipStreamDestroy(m->host_stream);
@@ -294,22 +346,21 @@ int gpu_multi_count(const MultiRender* m) { return m->n; }
 namespace {
 
 // Enqueue one frame (caller holds m->mu): renders, the gather, the un-permute into `out` (a
-// device pointer on the first device, ordered after `stream`'s prior work); `stream` waits for it.
+// device pointer on the first device) on `stream`, after its prior work.  `stream` is device 0's
+// comm stream for this frame.
 void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_t rng, uint32_t trace, float* out,
              hipStream_t stream) {
     const Rccl& r = rccl();
     ensure_buffers(m, p0.width, p0.height);
-    const int s = (int)(m->frames % PIPE);
+    const int s = (int)(m->frames % (uint64_t)m->pipe);    // buffer set
+    const int rsi = (int)(m->frames % (uint64_t)m->nrs);   // render stream
     const uint32_t N = (uint32_t)m->n;
-    {
-        Guard g(m->first);
-        hcheck(hipEventRecord(m->in_ev[s], stream), "hipEventRecord");
-    }
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
+        Guard g(m->dev_of(d));
         MultiRender::Dev& x = m->dev[(size_t)d];
-        // rows[s] is free once the gather of frame k - PIPE has read it
-        hcheck(hipStreamWaitEvent(x.rs[s], x.gathered[s], 0), "hipStreamWaitEvent");
+        hipStream_t rs = x.rs[rsi];
+        // rows[s] is free once the gather of frame k - pipe has read it
+        hcheck(hipStreamWaitEvent(rs, x.gathered[s], 0), "hipStreamWaitEvent");
         RenderParams q = p0;
         q.row_offset = (uint32_t)d;
         q.row_stride = N;
@@ -317,50 +368,77 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
         q.pixel_begin = 0;
         q.pixel_end = q.rows * q.width;
         q.out = x.rows[s];
-        hcheck(hipEventRecord(x.t0[s], x.rs[s]), "hipEventRecord");
+        hcheck(hipEventRecord(x.t0[s], rs), "hipEventRecord");
         if (d == 0) {
             if (!m->w_armed) {
-                hcheck(hipEventRecord(m->w0, x.rs[s]), "hipEventRecord");
+                hcheck(hipEventRecord(m->w0, rs), "hipEventRecord");
                 m->w_armed = true;
                 m->w_frames = 0;
             }
             ++m->w_frames;
         }
-        gpu_launch_render(m->scenes[(size_t)d], q, precision, rng, trace, x.rs[s]);
-        hcheck(hipEventRecord(x.t1[s], x.rs[s]), "hipEventRecord");
-        hcheck(hipEventRecord(x.rendered[s], x.rs[s]), "hipEventRecord");
-        hcheck(hipStreamWaitEvent(x.cs, x.rendered[s], 0), "hipStreamWaitEvent");
+        if (q.rows) gpu_launch_render(m->scenes[(size_t)d], q, precision, rng, trace, rs);
+        hcheck(hipEventRecord(x.t1[s], rs), "hipEventRecord");
+        hcheck(hipEventRecord(x.rendered[s], rs), "hipEventRecord");
+        hipStream_t cs = d == 0 ? stream : x.cs;
+        hcheck(hipStreamWaitEvent(cs, x.rendered[s], 0), "hipStreamWaitEvent");
+        // device 0's gathers run on the callers' streams: one that differs from the last frame's must
+        // not start this gather before the previous one (RCCL's per-communicator order)
+        if (d == 0 && m->last >= 0)
+            hcheck(hipStreamWaitEvent(cs, x.gathered[m->last], 0), "hipStreamWaitEvent");
     }
     {
         Guard g(m->first);
-        hcheck(hipEventRecord(m->g0[s], m->dev[0].cs), "hipEventRecord");
+        hcheck(hipEventRecord(m->g0[s], stream), "hipEventRecord");
     }
     const size_t count = (size_t)m->rows_max * m->W * 3;
-    ncheck(r.group_start(), "ncclGroupStart");
-    ncclResult_t gr = ncclSuccess;
-    for (int d = 0; d < m->n && gr == ncclSuccess; ++d) {
-        Guard g(m->first + d);  // (RCCL's group launch reads the current device)
-        gr = r.gather(m->dev[(size_t)d].rows[s], d == 0 ? m->staging[s] : nullptr, count, ncclFloat32, 0,
-                      m->comms[(size_t)d], m->dev[(size_t)d].cs);
+    if (m->loopback || m->n == 1) {  // shard d's "gather": its rows into staging slot d, on its comm stream
+        for (int d = 0; d < m->n; ++d) {
+            Guard g(m->first);
+            hcheck(hipMemcpyAsync(m->staging[s] + (size_t)d * count, m->dev[(size_t)d].rows[s], count * sizeof(float),
+                                  hipMemcpyDeviceToDevice, d == 0 ? stream : m->dev[(size_t)d].cs),
+                   "hipMemcpyAsync(loopback gather)");
+        }
+    } else {
+        ncheck(r.group_start(), "ncclGroupStart");
+        ncclResult_t gr = ncclSuccess;
+        for (int d = 0; d < m->n && gr == ncclSuccess; ++d) {
+            Guard g(m->dev_of(d));  // (RCCL's group launch reads the current device)
+            gr = r.gather(m->dev[(size_t)d].rows[s], d == 0 ? m->staging[s] : nullptr, count, ncclFloat32, 0,
+                          m->comms[(size_t)d], d == 0 ? stream : m->dev[(size_t)d].cs);
+        }
+        const ncclResult_t er = r.group_end();
+        ncheck(gr, "ncclGather");
+        ncheck(er, "ncclGroupEnd");
     }
-    const ncclResult_t er = r.group_end();
-    ncheck(gr, "ncclGather");
-    ncheck(er, "ncclGroupEnd");
     for (int d = 0; d < m->n; ++d) {
-        Guard g(m->first + d);
-        hcheck(hipEventRecord(m->dev[(size_t)d].gathered[s], m->dev[(size_t)d].cs), "hipEventRecord");
+        Guard g(m->dev_of(d));
+        hcheck(hipEventRecord(m->dev[(size_t)d].gathered[s], d == 0 ? stream : m->dev[(size_t)d].cs),
+               "hipEventRecord");
     }
     Guard g(m->first);
-    hipStream_t cs0 = m->dev[0].cs;
-    hcheck(hipStreamWaitEvent(cs0, m->in_ev[s], 0), "hipStreamWaitEvent");  // `out` is the caller's
-    hipLaunchKernelGGL(unpermute_rows, dim3(m->H), dim3(256), 0, cs0, (const float*)m->staging[s], out, N,
+    // RCCL's root completes its gather once every shard has arrived; the loopback copies of the other
+    // shards ran on their own comm streams
+    if (m->loopback)
+        for (int d = 1; d < m->n; ++d)
+            hcheck(hipStreamWaitEvent(stream, m->dev[(size_t)d].gathered[s], 0), "hipStreamWaitEvent");
+    hipLaunchKernelGGL(unpermute_rows, dim3(m->H), dim3(256), 0, stream, (const float*)m->staging[s], out, N,
                        m->rows_max, m->W * 3u);
     hcheck(hipGetLastError(), "un-permute launch");
-    hcheck(hipEventRecord(m->g1[s], cs0), "hipEventRecord");
-    hcheck(hipEventRecord(m->done_ev[s], cs0), "hipEventRecord");
-    hcheck(hipStreamWaitEvent(stream, m->done_ev[s], 0), "hipStreamWaitEvent");
+    hcheck(hipEventRecord(m->g1[s], stream), "hipEventRecord");
     m->last = s;
     ++m->frames;
+}
+
+// The caller's stream must belong to the first device (the null stream: the first device's).
+void check_stream(const MultiRender* m, hipStream_t stream) {
+    if (!stream) return;
+    hipDevice_t d = -1;
+    hcheck(hipStreamGetDevice(stream, &d), "hipStreamGetDevice");
+    if ((int)d != m->first)
+        throw std::invalid_argument("gpus >= 1: hip_stream belongs to device " + std::to_string((int)d) +
+                                    ", the frame to device " + std::to_string(m->first) +
+                                    " (opts.device; -1 = device 0)");
 }
 
 }  // namespace
@@ -368,6 +446,7 @@ void enqueue(MultiRender* m, const RenderParams& p0, uint32_t precision, uint32_
 void gpu_multi_render_device(MultiRender* m, const RenderParams& p, uint32_t precision, uint32_t rng, uint32_t trace,
                              float* dev_out, void* stream) {
     std::lock_guard<std::mutex> lock(m->mu);
+    check_stream(m, (hipStream_t)stream);
     enqueue(m, p, precision, rng, trace, dev_out, (hipStream_t)stream);
 }
 
@@ -390,7 +469,7 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
     for (int d = 0; d <= m->n + 1; ++d) {
         float ms = 0.0f;
         if (d < m->n) {
-            Guard g(m->first + d);
+            Guard g(m->dev_of(d));
             hcheck(hipEventSynchronize(m->dev[(size_t)d].t1[s]), "hipEventSynchronize");
             hcheck(hipEventElapsedTime(&ms, m->dev[(size_t)d].t0[s], m->dev[(size_t)d].t1[s]), "hipEventElapsedTime");
         } else if (d == m->n) {
@@ -406,6 +485,17 @@ size_t gpu_multi_timings(MultiRender* m, float* out, size_t n) {
     }
     if (n > (size_t)m->n + 1) m->w_armed = false;  // read: the next frame opens a new window (a size query keeps it)
     return (size_t)m->n + 2;
+}
+
+void gpu_multi_prepare(MultiRender* m, uint32_t width, uint32_t height) {
+    std::lock_guard<std::mutex> lock(m->mu);
+    ensure_buffers(m, width, height);
+}
+
+bool gpu_multi_rccl_usable(std::string* why) {
+    const Rccl& r = rccl();
+    if (!r.ok && why) *why = r.why;
+    return r.ok;
 }
 
 }  // namespace nrt

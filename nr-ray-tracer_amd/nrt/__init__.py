@@ -120,6 +120,7 @@ SIGNATURES = {
                              C.c_size_t, PROGRESS_FN, C.c_void_p]),
     "nrt_render_device": (C.c_int, [C.c_void_p, C.POINTER(_Camera), C.POINTER(_RenderOpts), C.c_void_p, C.c_size_t,
                                     C.c_void_p]),
+    "nrt_render_prepare": (C.c_int, [C.c_void_p, C.POINTER(_Camera), C.POINTER(_RenderOpts)]),
     "nrt_render_timings": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_size_t)]),
     "nrt_rows_selected": (C.c_uint32, [C.c_uint32, C.POINTER(_RenderOpts)]),
     "nrt_scene_upload": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -457,6 +458,14 @@ class Scene:
         _check(lib().nrt_render_device(self._h, C.byref(cam._c()), C.byref(o), C.c_void_p(out_ptr), out_len,
                                        C.c_void_p(stream)))
 
+
+    def prepare(self, camera: Optional[Camera] = None, precision: str = "f32", rng: str = "philox",
+                device: int = -1, trace: str = "auto", gpus: int = 0) -> None:
+        """nrt_render_prepare: the uploads and, with gpus = N >= 1, the RCCL communicators and shard
+        buffers of such a render, done now (NrtError code -4 when librccl cannot gather)."""
+        cam = camera or self.camera
+        o = _opts(precision, rng, device, 0, 1, trace, gpus)
+        _check(lib().nrt_render_prepare(self._h, C.byref(cam._c()), C.byref(o)))
 
     def render_timings(self) -> dict:
         """HIP-event times of the last gpus >= 1 render (nrt_render_timings): per-device render launch ms,

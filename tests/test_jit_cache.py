@@ -60,3 +60,47 @@ def test_damaged_cache_file_is_rebuilt(tmp_path):
     assert again["sha"] == first["sha"]
     third = _run(tmp_path)  # the rebuilt file is whole again
     assert third["disk_hits"] == 1 and third["sha"] == first["sha"]
+
+
+def test_untrusted_cache_directory_is_not_used(tmp_path):
+    """A cache directory other users may write (here world-writable) could hand this process someone
+    else's GPU code: the library neither reads nor writes it, and compiles in the process instead."""
+    d = tmp_path / "shared"
+    d.mkdir()
+    os.chmod(d, 0o777)
+    first = _run(d)
+    assert first["compiled"] == 1 and first["disk_hits"] == 0 and first["failed"] == 0
+    assert glob.glob(str(d / "*.co")) == []
+    second = _run(d)
+    assert second["compiled"] == 1 and second["disk_hits"] == 0 and second["sha"] == first["sha"]
+
+
+def _fnv1a(data, h=1469598103934665603):
+    for b in data:
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_cache_file_the_runtime_refuses_is_replaced(tmp_path):
+    """A cache file whose key and checksum hold but whose code object the HIP runtime refuses (another
+    compiler's output, say) is deleted and compiled once more in the same process: the render uses the
+    scene-specialised kernel, and the next process reads the rewritten file."""
+    import struct
+    first = _run(tmp_path)
+    (path,) = glob.glob(str(tmp_path / "*.co"))
+    buf = open(path, "rb").read()
+    at = 8
+    (klen,) = struct.unpack_from("<I", buf, at)
+    at += 4 + klen
+    (nlen,) = struct.unpack_from("<I", buf, at)
+    at += 4 + nlen
+    (clen,) = struct.unpack_from("<Q", buf, at)
+    at += 8
+    bad = bytearray(buf[:at]) + (b"not a code object " * (clen // 18 + 1))[:clen]
+    bad += struct.pack("<Q", _fnv1a(bytes(bad)))
+    open(path, "wb").write(bytes(bad))
+    again = _run(tmp_path)
+    assert again["disk_hits"] == 1 and again["compiled"] == 1 and again["failed"] == 0
+    assert again["launches"] >= 1 and again["sha"] == first["sha"]
+    third = _run(tmp_path)
+    assert third["disk_hits"] == 1 and third["compiled"] == 0 and third["sha"] == first["sha"]

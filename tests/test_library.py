@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nrt.lib().nrt_abi_version() == 6
+    assert nrt.lib().nrt_abi_version() == 7
 
 
 def test_camera_builder_default_and_build():
@@ -220,3 +220,26 @@ def test_chacha8_probe_streams_below_2_32():
     with pytest.raises(nrt.NrtError) as ei:
         nrt.debug_rng("chacha8", 2 ** 32 - 8, 64, 4)
     assert ei.value.code == -1 and "2^32" in str(ei.value)
+
+
+def test_bench_refuses_multi_gpu_loopback():
+    """NRT_MULTI_LOOPBACK (the library's test-only N-shards-on-one-GPU mode) never produces a bench line."""
+    import subprocess
+    import sys
+    env = dict(os.environ, NRT_MULTI_LOOPBACK="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], capture_output=True, text=True,
+                       env=env, timeout=60)
+    assert r.returncode != 0 and "NRT_MULTI_LOOPBACK" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_render_prepare_without_gpu_is_a_device_error():
+    """nrt_render_prepare (ABI 7) reports a missing GPU as NRT_E_DEVICE, like the render calls."""
+    if nrt.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    b = nrt.Builder()
+    m = b.lambertian(b.solid((0.5, 0.5, 0.5)))
+    s = b.finish(b.bvh([b.sphere((0, 0, 0), 0.5, m)]), nrt.CameraBuilder(width=4, height=4).build())
+    with pytest.raises(nrt.NrtError) as e:
+        s.prepare(gpus=2)
+    assert e.value.code == -3

@@ -7,8 +7,12 @@ Philox pixel sums are exact.
   * gloo, two processes sharing cuda:0 (runs on any GPU box: the shard renders of
     several processes on the same card, the host-side gather bench.py's code uses);
   * the library's own multi-GPU render in one process (nrt_render_opts.gpus, csrc/multi.hip:
-    ncclCommInitAll + one ncclGather per frame): through the RCCL code at N = 1 on any box, at
-    N >= 2 where the devices exist.
+    ncclCommInitAll + one ncclGather per frame): at N = 1 on any box (a communicator of one has
+    nothing to exchange: the gather is a device copy), through RCCL at N >= 2 where the devices
+    exist, and at N = 2, 3, 8 on one GPU through the test-only loopback
+    (NRT_MULTI_LOOPBACK=1: the N shards on GPU 0, each shard's ncclGather a device-to-device copy
+    into the same staging slot; the row counts, short shards, buffer-set rotation, event chaining
+    and un-permute are the N-GPU code).
 
 The launcher (torch.distributed.run) is a child process: nothing here execs.
 """
@@ -113,9 +117,10 @@ def test_bench_without_launcher_starts_its_ranks():
 
 
 @pytest.mark.parametrize("precision,rng", VARIANTS)
-def test_library_multi_gpu_n1_through_rccl(precision, rng):
-    """nrt_render_opts.gpus = 1: the frame goes through the library's RCCL path (communicator of one,
-    ncclGather to itself, the row un-permute) and equals the single-device render bit for bit."""
+def test_library_multi_gpu_n1(precision, rng):
+    """nrt_render_opts.gpus = 1: the frame goes through the library's multi-GPU path (buffer sets, the
+    shard's copy into the staging buffer, the row un-permute) and equals the single-device render bit
+    for bit."""
     with in_golden():
         s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
     want = s.render(precision=precision, rng=rng, device=0)
@@ -142,8 +147,8 @@ def test_library_multi_gpu_device_api_pipelined():
 
 
 def test_bench_library_path_n1_matches_single():
-    """bench.py --multi library (one process, the library's RCCL path) renders the frame of the default
-    single-device path."""
+    """bench.py --multi library (one process, the library's multi-GPU path) renders the frame of the
+    default single-device path."""
     one = _bench(1)
     lib1 = _bench(1, ("--multi", "library"))
     assert lib1["multi_gpu"]["path"] == "library" and lib1["n_gpus"] == 1
@@ -195,3 +200,72 @@ def test_render_on_second_device_keeps_current_device():
     got = s.render(precision="f64", rng="chacha8", device=1)
     assert torch.cuda.current_device() == 0
     np.testing.assert_array_equal(got, want)
+
+
+LOOPBACK_N = (2, 3, 8)
+
+
+@pytest.mark.parametrize("precision,rng", VARIANTS)
+def test_library_multi_gpu_loopback_bitwise_identical(monkeypatch, precision, rng):
+    """The library's N-GPU render (multi.hip) at N = 2, 3, 8 on one GPU (loopback): H = 37 leaves the last
+    shards a row short at every N, and a 5-row frame leaves shards 5..7 of N = 8 empty; every frame equals
+    the single-device render bit for bit (camera.rs:318-320: a pixel's value is a function of its index)."""
+    monkeypatch.setenv("NRT_MULTI_LOOPBACK", "1")
+    for h in (H, 5):
+        with in_golden():
+            s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=h, samples_per_pixel=SPP))
+        want = s.render(precision=precision, rng=rng, device=0)
+        for g in LOOPBACK_N:
+            got = s.render(precision=precision, rng=rng, device=0, gpus=g)
+            np.testing.assert_array_equal(got, want, err_msg=f"gpus={g} H={h}")
+            t = s.render_timings()
+            assert len(t["kernel_ms"]) == g and t["gather_ms"] > 0
+
+
+def test_library_multi_gpu_loopback_device_api_pipelined(monkeypatch):
+    """nrt_render_device with gpus = 3 (loopback), seven frames enqueued back to back, alternating between
+    two caller streams (GPU 0's gathers run on the caller's stream, chained to the previous frame's gather
+    when it changes), then a different frame size (the shard buffers are re-made): every frame equals the
+    single-device render."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("NRT_MULTI_LOOPBACK", "1")
+    with in_golden():
+        s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
+    want = s.render(precision="f32", rng="philox", device=0)
+    s.prepare(precision="f32", rng="philox", device=0, gpus=3)
+    streams = [torch.cuda.Stream(device=0), torch.cuda.current_stream(0)]
+    outs = [torch.full((H, W, 3), -1.0, dtype=torch.float32, device="cuda:0") for _ in range(7)]
+    for k, o in enumerate(outs):
+        s.render_device(o.data_ptr(), o.numel(), precision="f32", rng="philox", device=0,
+                        stream=streams[k % 2].cuda_stream, gpus=3)
+    torch.cuda.synchronize(0)
+    for k, o in enumerate(outs):
+        np.testing.assert_array_equal(o.cpu().numpy(), want, err_msg=f"frame {k}")
+    t = s.render_timings()
+    assert len(t["kernel_ms"]) == 3 and t["period_ms"] > 0
+    import dataclasses
+    small = dataclasses.replace(s.camera, height=16)
+    o = torch.empty((16, W, 3), dtype=torch.float32, device="cuda:0")
+    s.render_device(o.data_ptr(), o.numel(), camera=small, precision="f32", rng="philox", device=0,
+                    stream=streams[0].cuda_stream, gpus=3)
+    torch.cuda.synchronize(0)
+    np.testing.assert_array_equal(o.cpu().numpy(), s.render(small, precision="f32", rng="philox", device=0))
+
+
+def test_library_multi_gpu_prepare_and_stream_checks(monkeypatch):
+    """nrt_render_prepare builds the N-GPU context before the first render (N = 1, loopback at N = 8); a
+    caller stream of another device is NRT_E_INVALID (>= 2 GPUs)."""
+    torch = pytest.importorskip("torch")
+    with in_golden():
+        s = nrt.Scene.load(SCENE, nrt.CameraConfig(width=W, height=H, samples_per_pixel=SPP))
+    s.prepare(precision="f32", rng="philox", device=0, gpus=1)
+    monkeypatch.setenv("NRT_MULTI_LOOPBACK", "1")
+    s.prepare(precision="f32", rng="philox", device=0, gpus=8)
+    monkeypatch.delenv("NRT_MULTI_LOOPBACK")
+    with pytest.raises(nrt.NrtError):
+        s.prepare(device=0, gpus=nrt.device_count() + 1)  # more devices than visible
+    if nrt.device_count() >= 2:
+        other = torch.cuda.Stream(device=1)
+        o = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+        with pytest.raises(nrt.NrtError, match="belongs to device 1"):
+            s.render_device(o.data_ptr(), o.numel(), device=0, stream=other.cuda_stream, gpus=1)
