@@ -351,6 +351,11 @@ void check_opts(const nrt_render_opts* o) {
 
 // NRT_MULTI_LOOPBACK=1 (tests only): a gpus = N render runs its N row shards on the first device,
 // the gather as device-to-device copies (multi.hip), so the N-GPU code runs on a one-GPU box
+// Philox groups per resident wave of a synchronous nrt_render (RenderParams::groups_per_wave): its
+// launch's tail is not overlapped by a next one, and smaller last groups shorten it (C5 row shards at
+// N = 8 unpipelined: 0.830 of linear with 4, 0.872 with 16, profiles/r05_shard_scaling_c5.json)
+constexpr uint32_t ONE_SHOT_GROUPS_PER_WAVE = 16;
+
 bool multi_loopback() {
     const char* e = std::getenv("NRT_MULTI_LOOPBACK");
     return e && *e && std::strcmp(e, "0") != 0;
@@ -651,6 +656,7 @@ int nrt_render(const nrt_scene* scene, const nrt_camera* camera, const nrt_rende
         const size_t n = (size_t)rows * p.width * 3;
         if (out_len < n) throw std::invalid_argument("output buffer too small");
         if (n == 0) return NRT_OK;
+        p.groups_per_wave = ONE_SHOT_GROUPS_PER_WAVE;  // a one-shot render: nothing follows to fill its tail
         if (opts && opts->gpus) {  // the whole frame over opts->gpus devices, one RCCL gather
             MultiRender* m = multi_render(const_cast<nrt_scene*>(scene), opts);
             gpu_multi_render_host(m, p, opts->precision, opts->rng, opts->trace, out_rgb);

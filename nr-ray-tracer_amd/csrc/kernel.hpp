@@ -84,6 +84,14 @@ constexpr int BLOCK = NRT_BLOCK;
 #ifndef NRT_WALK_CONTRACT
 #define NRT_WALK_CONTRACT 1  // FMA contraction in the exact kernel's f32 culling walk and prefilter
 #endif
+#ifndef NRT_BOX_DEFER
+// world list: 1 = a box unit's (PRIM_BOX / PRIM_BOXY) face is resolved once, for the winner of the whole
+// run loop, instead of per unit and ray (the unit keeps (t, its index, entry / exit)).  Measured on C5
+// (round 6, 3 alternating runs, frames identical): 9.81-9.82 ms per frame with the face per unit, 10.69-
+// 10.71 ms deferred (-9 %): the winner's record comes by per-lane vector loads in a divergent branch
+// after the loop, where the per-unit selects ride on scalar-loaded records; off
+#define NRT_BOX_DEFER 0
+#endif
 #ifndef NRT_CHACHA_TOPUP
 #define NRT_CHACHA_TOPUP 1  // ChaCha8 ring refilled at the persistent loop's head (ChaCha8::top_up)
 #endif
@@ -99,8 +107,8 @@ constexpr uint32_t CHACHA_LDS_BYTES = RING * BLOCK * 8u + 3u * BLOCK * 8u;
 constexpr uint32_t STG_SLOTS = 8, STG_PX = 8, NO_STG = 0xFFFFFFFFu;
 constexpr uint32_t STG_WAVE_WORDS = STG_SLOTS * (STG_PX * 3u + 3u);
 constexpr uint32_t STG_LDS_BYTES = (BLOCK / 64u) * STG_WAVE_WORDS * 4u;
-__host__ __device__ inline uint32_t chacha_lds_bytes(uint32_t exact_claim) {
-    return CHACHA_LDS_BYTES + (exact_claim > 1u ? STG_LDS_BYTES : 0u);
+__host__ __device__ inline uint32_t chacha_lds_bytes(uint32_t exact_stage) {
+    return CHACHA_LDS_BYTES + (exact_stage ? STG_LDS_BYTES : 0u);
 }
 
 template <typename R>
@@ -888,6 +896,85 @@ __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t
     }
 }
 
+// Box units (PRIM_BOXY, PRIM_BOX): the slab planes' t along the ray per axis (a*: plane l = D,
+// b*: l = D + L) and the local reciprocals that give the entry sides.  One definition serves the run
+// loop and the deferred face resolution (NRT_BOX_DEFER), so both round alike (-ffp-contract=on fuses
+// by expression: the same source, the same FMAs).
+struct BoxPlanes {
+    float ax, bx, ay, by, az, bz;
+    float ix, iy, iz;  // local 1/d' (BOXY: iy unused, its y axis is the world's)
+};
+__device__ __forceinline__ BoxPlanes boxy_planes(ConstPrimWorld<float> q, const f32x2& dox, const f32x2& doz,
+                                                 const float inv[3], const float oinv[3]) {
+    BoxPlanes b;
+    const f32x2 la = dox * q->N[0] + doz * q->N[2];  // (row_A . d, row_A . o)
+    const f32x2 lb = dox * q->AB[0] + doz * q->AB[2];
+    b.ix = __builtin_amdgcn_rcpf(la.x);
+    b.iz = __builtin_amdgcn_rcpf(lb.x);
+    b.iy = 0.0f;
+    b.ax = (q->D - la.y) * b.ix;
+    b.az = (q->AB[3] - lb.y) * b.iz;
+    b.bx = __builtin_fmaf(q->D - la.y, b.ix, b.ix);
+    b.bz = __builtin_fmaf(q->AB[3] - lb.y, b.iz, b.iz);
+    b.ay = __builtin_fmaf(q->AB[4], inv[1], -oinv[1]);
+    b.by = __builtin_fmaf(q->AB[5], inv[1], -oinv[1]);
+    return b;
+}
+__device__ __forceinline__ BoxPlanes box_planes(ConstPrimWorld<float> q, const f32x2& dox, const f32x2& doy,
+                                                const f32x2& doz) {
+    BoxPlanes b;
+    // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
+    const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
+    const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
+    const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
+    b.ix = __builtin_amdgcn_rcpf(lx.x);
+    b.iy = __builtin_amdgcn_rcpf(ly.x);
+    b.iz = __builtin_amdgcn_rcpf(lz.x);
+    // planes l = D and l = D + L per local axis (L_a in S[a]; flatten.cpp fuse_box)
+    b.ax = (q->D - lx.y) * b.ix;
+    b.ay = (q->AB[3] - ly.y) * b.iy;
+    b.az = (q->AB[7] - lz.y) * b.iz;
+    b.bx = __builtin_fmaf(q->D - lx.y, b.ix, b.ix);
+    b.by = __builtin_fmaf(q->AB[3] - ly.y, b.iy, b.iy);
+    b.bz = __builtin_fmaf(q->AB[7] - lz.y, b.iz, b.iz);
+    return b;
+}
+// The face quad (0-5, the unit's record + 1 + face) through which the ray enters (entry) or leaves
+// the box: face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0), the
+// quad that lies there from 3 bits per slot of meta.  sy: BOXY's y slot pair from the world ray.
+__device__ __forceinline__ uint32_t box_face(const BoxPlanes& b, uint32_t meta, bool entry, uint32_t sy) {
+    const float nx = fminf(b.ax, b.bx), ny = fminf(b.ay, b.by), nz = fminf(b.az, b.bz);
+    const float fx = fmaxf(b.ax, b.bx), fy = fmaxf(b.ay, b.by), fz = fmaxf(b.az, b.bz);
+    const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+    const uint32_t sx = b.ix < 0.0f ? 1u : 0u, sz = b.iz < 0.0f ? 5u : 4u;
+    uint32_t se = sz, sxit = sz ^ 1u;
+    se = tn == ny ? sy : se;
+    se = tn == nx ? sx : se;
+    sxit = tf == fy ? sy ^ 1u : sxit;
+    sxit = tf == fx ? sx ^ 1u : sxit;
+    const uint32_t slot = entry ? se : sxit;
+    return __builtin_amdgcn_ubfe(meta, WKIND_BITS + 3u * slot, 3);
+}
+// best of a box unit whose face is resolved after the run loop (NRT_BOX_DEFER): the unit's index |
+// WBEST_BOX (| WBEST_BOXY for a box turned about y) | WBEST_ENTRY (the ray enters at t)
+constexpr uint32_t WBEST_BOX = 1u << 30, WBEST_BOXY = 1u << 29, WBEST_ENTRY = 1u << 28;
+template <bool BOX = true, bool BOXY = true>  // the box kinds the scene's world list holds
+__device__ __forceinline__ int32_t resolve_box_face(ConstPrimWorld<float> wp, int32_t best, const f32x2& dox,
+                                                    const f32x2& doy, const f32x2& doz, const float inv[3],
+                                                    const float oinv[3], const uint32_t entry_slot[3]) {
+    const uint32_t k = (uint32_t)best & (WBEST_ENTRY - 1u);
+    const ConstPrimWorld<float> q = wp + k;
+    const bool entry = ((uint32_t)best & WBEST_ENTRY) != 0u;
+    uint32_t face = 0;
+    if (BOXY && (!BOX || ((uint32_t)best & WBEST_BOXY))) {
+        face = box_face(boxy_planes(q, dox, doz, inv, oinv), q->meta, entry, entry_slot[1]);
+    } else if (BOX) {
+        const BoxPlanes b = box_planes(q, dox, doy, doz);
+        face = box_face(b, q->meta, entry, b.iy < 0.0f ? 3u : 2u);
+    }
+    return (int32_t)(k + 1u + face);
+}
+
 // The units of one run (kind = the run's kind): closest hit so far in (t_best, best).
 // `t <= t_best`: the later candidate wins an exact tie (the flattener orders the units
 // so that this is the reference's winner of every coplanar tie, device_scene.hpp WCLASS_*).
@@ -929,65 +1016,40 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
     if (kind == PRIM_BOXY) {  // box turned about y: two local rows + the world y slab
         for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
             const ConstPrimWorld<float> q = wp + k;
-            const f32x2 la = dox * q->N[0] + doz * q->N[2];  // (row_A . d, row_A . o)
-            const f32x2 lb = dox * q->AB[0] + doz * q->AB[2];
-            const float ia = __builtin_amdgcn_rcpf(la.x), ib = __builtin_amdgcn_rcpf(lb.x);
-            const float ax = (q->D - la.y) * ia, az = (q->AB[3] - lb.y) * ib;
-            const float bx = __builtin_fmaf(q->D - la.y, ia, ia), bz = __builtin_fmaf(q->AB[3] - lb.y, ib, ib);
-            const float ay = __builtin_fmaf(q->AB[4], inv[1], -oinv[1]), by = __builtin_fmaf(q->AB[5], inv[1], -oinv[1]);
-            const float nx = fminf(ax, bx), ny = fminf(ay, by), nz = fminf(az, bz);
-            const float fx = fmaxf(ax, bx), fy = fmaxf(ay, by), fz = fmaxf(az, bz);
+            const BoxPlanes bp = boxy_planes(q, dox, doz, inv, oinv);
+            const float nx = fminf(bp.ax, bp.bx), ny = fminf(bp.ay, bp.by), nz = fminf(bp.az, bp.bz);
+            const float fx = fmaxf(bp.ax, bp.bx), fy = fmaxf(bp.ay, bp.by), fz = fmaxf(bp.az, bp.bz);
             const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
             const bool entry = tn >= 0.001f;
             const float t = entry ? tn : tf;
             // = (tn <= tf) & (t >= 0.001) & (t <= t_best): an entry t is >= 0.001 by choice,
             // an exit t = tf (tn < 0.001 <= tf then orders the slab)
             const bool ok = (t <= fminf(tf, t_best)) & (t >= 0.001f);
-            const uint32_t sx = ia < 0.0f ? 1u : 0u, sz = ib < 0.0f ? 5u : 4u;
-            uint32_t se = sz, sxit = sz ^ 1u;
-            se = tn == ny ? entry_slot[1] : se;
-            se = tn == nx ? sx : se;
-            sxit = tf == fy ? entry_slot[1] ^ 1u : sxit;
-            sxit = tf == fx ? sx ^ 1u : sxit;
-            const uint32_t slot = entry ? se : sxit;
-            const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
             t_best = ok ? t : t_best;
-            best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
+#if NRT_BOX_DEFER
+            best = ok ? (int32_t)(k | WBEST_BOX | WBEST_BOXY | (entry ? WBEST_ENTRY : 0u)) : best;
+#else
+            best = ok ? (int32_t)(k + 1 + box_face(bp, q->meta, entry, entry_slot[1])) : best;  // the face quad's record
+#endif
         }
         return;
     }
     if (kind == PRIM_BOX) {  // fused parallelepiped: one slab test in its local frame
         for (uint32_t b = 0; b < count; ++b, k += BOX_ENTRIES) {
             const ConstPrimWorld<float> q = wp + k;
-            // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
-            const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
-            const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
-            const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
-            const float ix = __builtin_amdgcn_rcpf(lx.x), iy = __builtin_amdgcn_rcpf(ly.x),
-                        iz = __builtin_amdgcn_rcpf(lz.x);
-            const float ax = (q->D - lx.y) * ix, ay = (q->AB[3] - ly.y) * iy, az = (q->AB[7] - lz.y) * iz;
-            // planes l = D and l = D + L per local axis (L_a in S[a]; flatten.cpp fuse_box)
-            // planes x' = 0 and x' = 1
-            const float bx = __builtin_fmaf(q->D - lx.y, ix, ix), by = __builtin_fmaf(q->AB[3] - ly.y, iy, iy),
-                        bz = __builtin_fmaf(q->AB[7] - lz.y, iz, iz);
-            const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-            const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+            const BoxPlanes bp = box_planes(q, dox, doy, doz);
+            const float tn = fmaxf(fmaxf(fminf(bp.ax, bp.bx), fminf(bp.ay, bp.by)), fminf(bp.az, bp.bz));
+            const float tf = fminf(fminf(fmaxf(bp.ax, bp.bx), fmaxf(bp.ay, bp.by)), fmaxf(bp.az, bp.bz));
             // entry face unless it lies before t_min (origin on or inside the box): then the exit face
             const bool entry = tn >= 0.001f;
             const float t = entry ? tn : tf;
             const bool ok = (t <= fminf(tf, t_best)) & (t >= 0.001f);  // (as PRIM_BOXY)
-            // face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0),
-            // then the quad that lies there (3 bits per slot in meta)
-            const uint32_t sx = ix < 0.0f ? 1u : 0u, sy = iy < 0.0f ? 3u : 2u, sz = iz < 0.0f ? 5u : 4u;
-            uint32_t se = sz, sxit = sz ^ 1u;
-            se = tn == fminf(ay, by) ? sy : se;
-            se = tn == fminf(ax, bx) ? sx : se;
-            sxit = tf == fmaxf(ay, by) ? sy ^ 1u : sxit;
-            sxit = tf == fmaxf(ax, bx) ? sx ^ 1u : sxit;
-            const uint32_t slot = entry ? se : sxit;
-            const uint32_t face = __builtin_amdgcn_ubfe(q->meta, WKIND_BITS + 3u * slot, 3);
             t_best = ok ? t : t_best;
-            best = ok ? (int32_t)(k + 1 + face) : best;  // the face quad's record
+#if NRT_BOX_DEFER
+            best = ok ? (int32_t)(k | WBEST_BOX | (entry ? WBEST_ENTRY : 0u)) : best;
+#else
+            best = ok ? (int32_t)(k + 1 + box_face(bp, q->meta, entry, bp.iy < 0.0f ? 3u : 2u)) : best;
+#endif
         }
         return;
     }
@@ -1042,6 +1104,8 @@ struct NoSig {
 template <uint32_t... RUNS>
 struct WorldSig {
     static constexpr uint32_t n = sizeof...(RUNS);
+    template <uint32_t KIND>
+    static constexpr bool has() { return ((((RUNS & WRUN_KIND_MASK) == KIND) || ...)); }
     static constexpr int bvh = 0;
     static constexpr bool tie = false;
     static constexpr int prims = 0;
@@ -1119,6 +1183,11 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     uint32_t k = 0;
     if constexpr (SIG::n > 0) {  // a scene-specialised kernel (jit.hip): runs known at compile time
         sig_runs<FLAT>(SIG{}, wp, k, ray, dox, doy, doz, inv, oinv, entry_slot, t_best, best);
+#if NRT_BOX_DEFER
+        if (best >= 0 && ((uint32_t)best & WBEST_BOX))
+            best = resolve_box_face<SIG::template has<PRIM_BOX>(), SIG::template has<PRIM_BOXY>()>(wp, best, dox, doy, doz,
+                                                                                               inv, oinv, entry_slot);
+#endif
         hm.t = t_best;
         hm.prim = (uint32_t)best;
         hm.depth = 0;
@@ -1129,6 +1198,9 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
         const uint32_t kind = run & WRUN_KIND_MASK, count = run >> WRUN_KIND_BITS;
         world_run<FLAT>(wp, kind, k, count, ray, dox, doy, doz, inv, oinv, entry_slot, t_best, best);
     }
+#if NRT_BOX_DEFER
+    if (best >= 0 && ((uint32_t)best & WBEST_BOX)) best = resolve_box_face(wp, best, dox, doy, doz, inv, oinv, entry_slot);
+#endif
     hm.t = t_best;
     hm.prim = (uint32_t)best;
     hm.depth = 0;
@@ -2899,7 +2971,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     };
     // dynamic LDS: [ChaCha8 ring + pixel sums (+ claim staging) | Philox pool][world-BVH stack][staged scene]
     constexpr uint32_t ring_bytes = G::uses_lds ? RING * BLOCK * sizeof(uint2) : 0;
-    const uint32_t acc_bytes = G::exact_stream ? chacha_lds_bytes(p.exact_claim) - ring_bytes
+    const uint32_t acc_bytes = G::exact_stream ? chacha_lds_bytes(p.exact_stage) - ring_bytes
                                                : philox_pool_bytes<MAXD>(p.wave_pixels);
     // world-BVH stack (f32 kernels): the tree's bound + 1 entries (16-bit refs of the compact tree)
     using StackT = typename StackEntry<SIG::bvh == WBVH_COMPACT>::type;
@@ -3049,7 +3121,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             s = 0;
         };
         // claim staging (STG_SLOTS): this wave's slots, each STG_PX x 3 floats then (left, first, size)
-        const bool staging = p.exact_claim > 1u;  // (host: the LDS holds the slots only then)
+        const bool staging = p.exact_stage != 0u;  // (host: the LDS holds the slots only then)
         uint32_t* const stg = (uint32_t*)(lds + ring_bytes + 3u * BLOCK * (uint32_t)sizeof(double)) + wv * STG_WAVE_WORDS;
         auto stg_meta = [&](uint32_t slot) { return stg + STG_SLOTS * STG_PX * 3u + slot * 3u; };
         uint32_t stg_free = (1u << STG_SLOTS) - 1u;  // uniform: free slots
@@ -3103,16 +3175,21 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         uint32_t qk = 0;  // counters found exhausted (wave-uniform; QUEUE_HEADS: no pixel left)
         // The wave's reservoir (uniform): pixels [rb, rb + rn) claimed but not yet started.  Lanes
         // free up one at a time, so a claim of only the lanes asking cost one counter atomic per
-        // pixel and a wait on its return; a claim takes at least p.exact_claim pixels (the host's
-        // pick by spp, render.hip) and later asks are served from the reservoir.
+        // pixel and a wait on its return (a device-scope atomic executes at memory: ~35 B of HBM
+        // writes each, C4 f64 at spp 256: 35 of its 55 MB per launch with claims of 1); a claim takes
+        // at least p.exact_claim pixels and later asks are served from the reservoir -- while the
+        // head has more than one round of its lanes' pixels left (left: what the last claim saw);
+        // then only what the lanes ask, so no reservoir holds pixels into the tail (guided claims)
         uint32_t rb = 0, rn = 0;
+        uint32_t left = 0xFFFFFFFFu;  // uniform: pixels the head had left after this wave's last claim
+        const uint32_t guide = gridDim.x * (BLOCK / QUEUE_HEADS);  // one round of a head's lanes
         auto next_pixel = [&](bool need) -> bool {  // uniform; true: this lane got a pixel
             const uint64_t m = __ballot(need);
             if (m == 0ull) return false;
             const uint32_t cnt = (uint32_t)__popcll(m);
             if (rn == 0 && qk < QUEUE_HEADS) {
-                const uint32_t want = max(cnt, p.exact_claim);
-                uint32_t base = 0, got = 0;
+                const uint32_t want = max(cnt, left > guide ? p.exact_claim : 1u);
+                uint32_t base = 0, got = 0, rest = 0;
                 if (leader()) {
                     for (; qk < QUEUE_HEADS; ++qk) {
                         const uint32_t xh = (xcc + qk) & (QUEUE_HEADS - 1u);
@@ -3123,12 +3200,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                         if (t < n) {
                             base = lo + t;
                             got = min(want, n - t);
+                            rest = qk == 0 ? n - t - got : 0u;  // (a head of another XCD: its tail)
                             break;
                         }
                     }
                 }
                 rb = __builtin_amdgcn_readfirstlane(base);
                 rn = __builtin_amdgcn_readfirstlane(got);
+                left = __builtin_amdgcn_readfirstlane(rest);
                 qk = __builtin_amdgcn_readfirstlane(qk);
                 rslot = NO_STG;
                 if (staging && rn != 0 && rn <= STG_PX && stg_free != 0u) {  // a staging slot for the claim

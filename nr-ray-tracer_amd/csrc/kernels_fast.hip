@@ -39,9 +39,11 @@ void launch_fast_jit(const RenderParams& p0, const DSceneView<float>& v, void* f
     const uint32_t stack = maxd == MODE_WORLD_BVH ? (v.wbvh_stack + 1u) * dev::BLOCK * stack_entry : 0u;
     if (rng == RNG_CHACHA8) {  // persistent lanes (launch_variant): ring + stack below the staged scene
         const uint32_t npix = p0.pixel_end - p0.pixel_begin;
-        const uint32_t lds = lds_fixed + dev::chacha_lds_bytes(p0.exact_claim) + stack;
+        uint32_t lds = lds_fixed + dev::chacha_lds_bytes(p0.exact_stage) + stack;
+        RenderParams p = p0;
+        exact_stage_fit(p, lds, resident);
         const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
-        launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({need, resident(lds), chacha_grid_cap()})), lds, p0);
+        launch((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({need, resident(lds), chacha_grid_cap()})), lds, p);
         return;
     }
     if (maxd == MODE_WORLD_BVH)  // below the staged scene: the traversal stack (launch_one's ring)

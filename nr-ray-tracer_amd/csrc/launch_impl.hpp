@@ -86,7 +86,7 @@ static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&&
         // finish set the tail of a lone launch (C5 at N = 8 without pipelining: 4.6 -> 9.1
         // groups per wave, -5 % kernel time, round 3); pipelined launches overlap that tail
         auto groups = [&](uint32_t w) { return (uint64_t)(npix + w - 1) / w; };
-        uint64_t gpw = NRT_GROUPS_PER_WAVE;  // knob NRT_GROUPS_PER_WAVE (A/B runs)
+        uint64_t gpw = p.groups_per_wave ? p.groups_per_wave : NRT_GROUPS_PER_WAVE;  // knob NRT_GROUPS_PER_WAVE (A/B runs)
         if (const char* e = std::getenv("NRT_GROUPS_PER_WAVE")) {
             const long v = std::strtol(e, nullptr, 10);
             if (v >= 1 && v <= 64) gpw = (uint64_t)v;
@@ -103,15 +103,41 @@ static void philox_launch(const RenderParams& p0, uint32_t lds_fixed, Resident&&
     launch(blocks, lds_fixed + ring_bytes(wp), p);
 }
 
+// Persistent lanes: the claim staging (RenderParams::exact_stage) only where its LDS leaves the
+// resident workgroups unchanged.  C4 f64 (teapot: the 16-bit culling stack in LDS, 3 workgroups per CU)
+// lost one workgroup per CU to it: claims of 2 / 4 pixels measured 130.7 -> 153 ms in round 5, the
+// occupancy, not the claims.  `lds` includes the staging when p.exact_stage is set; both are updated.
+template <class Resident>
+static void exact_stage_fit(RenderParams& p, uint32_t& lds, Resident&& resident) {
+    const bool dbg = std::getenv("NRT_DEBUG_LAUNCH") != nullptr;  // (diagnostics: the launch's LDS and residency)
+    if (p.exact_stage) {
+        const uint32_t without = lds - dev::STG_LDS_BYTES;
+        const uint64_t with_b = resident(lds), without_b = resident(without);
+        if (dbg)
+            std::fprintf(stderr, "nrt: persistent lanes: LDS %u B -> %llu blocks resident, without claim staging %u B -> %llu\n",
+                         lds, (unsigned long long)with_b, without, (unsigned long long)without_b);
+        if (without_b > with_b) {
+            p.exact_stage = 0;
+            lds = without;
+        }
+    } else if (dbg) {
+        std::fprintf(stderr, "nrt: persistent lanes: LDS %u B -> %llu blocks resident (no claim staging)\n", lds,
+                     (unsigned long long)resident(lds));
+    }
+}
+
 // ChaCha8: one lane per pixel.
 template <typename R, class G, int MAXD, bool EXACT, bool LDS_SCENE, int KFLAGS, class SIG = dev::NoSig>
 static void launch_variant(const RenderParams& p0, const DSceneView<R>& v, uint32_t lds_fixed, hipStream_t stream) {
     auto kernel = dev::render_kernel<R, G, MAXD, EXACT, LDS_SCENE, KFLAGS, SIG>;
     const uint32_t npix = p0.pixel_end - p0.pixel_begin;
     if constexpr (G::exact_stream) {  // persistent lanes (render_kernel): the resident workgroups at most
+        RenderParams p = p0;
+        uint32_t lds = lds_fixed;
+        exact_stage_fit(p, lds, [&](uint32_t b) { return resident_blocks(kernel, b); });
         const uint64_t need = (npix + dev::BLOCK - 1) / dev::BLOCK;
-        const uint64_t blocks = std::max<uint64_t>(1, std::min({need, resident_blocks(kernel, lds_fixed), chacha_grid_cap()}));
-        hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(dev::BLOCK), lds_fixed, stream, p0, v);
+        const uint64_t blocks = std::max<uint64_t>(1, std::min({need, resident_blocks(kernel, lds), chacha_grid_cap()}));
+        hipLaunchKernelGGL(kernel, dim3((uint32_t)blocks), dim3(dev::BLOCK), lds, stream, p, v);
     } else {
         philox_launch<MAXD>(
             p0, lds_fixed, [&](uint32_t lds) { return resident_blocks(kernel, lds); },
@@ -126,7 +152,7 @@ static void launch_one(const RenderParams& p, const DSceneView<R>& v, bool perli
                        bool flat = false, bool planes = false) {
     // dynamic LDS below the staged scene: ChaCha8 ring or Philox group ring (added by
     // launch_variant), then the BVH stack
-    const uint32_t ring = (G::uses_lds ? dev::chacha_lds_bytes(p.exact_claim) : 0) +
+    const uint32_t ring = (G::uses_lds ? dev::chacha_lds_bytes(p.exact_stage) : 0) +
                           (MAXD < 0 ? (v.wbvh_stack + 1u) * dev::BLOCK * (uint32_t)sizeof(int32_t) : 0);
     const uint32_t scene = lds_scene_bytes(v, MAXD);
     using dev::KF_FLAT;

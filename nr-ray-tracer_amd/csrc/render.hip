@@ -265,10 +265,17 @@ void gpu_launch_render(const DeviceScene* ds, const RenderParams& p, uint32_t pr
         q.wave_wait = ds->flat ? 24u : 48u;  // 32 / 40: 31.2 / 31.3 against 30.9 ms, round 5), the sphere / texture variant at 48
                                              // (spheres.toml 1080p: 27.64 / 27.26 / 26.84 / 26.83 / 33.24 ms at 32 / 40 / 48 / 56 / 64)
                                              // (the exact kernel's persistent walk: its own default, launch_impl.hpp)
-    // Persistent lanes: claims of 128/spp pixels (1..8).  Short pixels end often, and a claim per
-    // finished pixel stalls the wave on the atomic's return (earth f64 spp 16: 6.26 -> 5.87 ms at
-    // 8); long ones hold the reservoir's pixels into the tail (C4 f64 spp 256: 191 -> 201 ms at 8).
-    if (q.exact_claim == 0) q.exact_claim = std::min(8u, std::max(1u, 128u / std::max(1u, q.spp)));
+    // Persistent lanes: claims of 8 pixels while the head has more than a round of its lanes' pixels
+    // left, then of what the lanes ask (kernel.hpp next_pixel).  A claim per finished pixel stalls the
+    // wave on the atomic's return (earth f64 spp 16: 6.26 -> 5.87 ms at 8) and writes ~35 B of HBM per
+    // atomic; the guided tail keeps a reservoir from holding pixels while other waves idle.  The staging
+    // of a claim's pixels in LDS, where it costs no occupancy (launch_impl.hpp exact_stage_fit).
+    // Staging only at spp <= 64: at spp 256 it measured C5 f64 169-170 -> 208 ms (claims of 8 either way;
+    // long pixels hold the wave's 8 slots) while saving no time at C4 / C5's pixel rates.
+    if (q.exact_claim == 0) q.exact_claim = 8u;
+    q.exact_stage = q.exact_claim > 1u && q.spp <= 64u ? 1u : 0u;
+    if (const char* e = std::getenv("NRT_EXACT_STAGE"))  // A/B knob: 0 = never stage claims in LDS
+        if (std::strtol(e, nullptr, 10) == 0) q.exact_stage = 0;
     {  // Philox: group queue heads; ChaCha8: the pixel counter of the persistent lanes (head 0)
         const size_t qwords = (size_t)QUEUE_HEADS * QUEUE_STRIDE;
         q.queue = ds->queues + (ds->queue_next.fetch_add(1) % QUEUE_SLOTS) * qwords;

@@ -84,10 +84,20 @@ struct RenderParams {
     // Exact world mode with the prefilter, at most EXACT_SLOTS_MAX slots: the prefilter over every
     // slot in order (scalar loads, no walk) instead of the culling walk (EXACT_SIG_SLOTS_PF).
     uint32_t exact_slots;
-    // Persistent lanes (ChaCha8): fewest pixels a wave claims per counter atomic; the rest wait in
+    // Persistent lanes (ChaCha8): fewest pixels a wave claims per counter atomic while its queue head
+    // has more than one round of the grid's lanes left (then as many as lanes ask); the rest wait in
     // the wave's reservoir (kernel.hpp next_pixel).  0: the host picks (render.hip).
     uint32_t exact_claim;
+    // Persistent lanes: a claim's finished pixels staged in LDS and written out as one run (1), or each
+    // pixel stored as it ends (0).  The host stages only where the staging LDS leaves the resident
+    // workgroups unchanged (launch_impl.hpp).
+    uint32_t exact_stage;
     float acc_scale_f;  // acc_scale in f32 (f32 kernels: k in [-126, 127])
+    // Philox group sizing (launch_impl.hpp philox_launch): groups per resident wave a launch keeps
+    // while groups hold > 512 samples; 0 = NRT_GROUPS_PER_WAVE (4, for streamed launches whose tail the
+    // next launch fills: nrt_render_device); nrt_render, a one-shot call, asks for 16 (smaller last
+    // groups shorten a lone launch's tail)
+    uint32_t groups_per_wave;
 };
 
 }  // namespace nrt

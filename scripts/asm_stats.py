@@ -62,6 +62,7 @@ def main():
     salu = sum(n for k, n in c.items() if k.startswith("s_"))
     print(f"{m.group(1)[:90]}\ninstructions {len(ins)}  valu {valu}  salu/branch {salu}")
     print("  ".join(f"{k} {n}" for k, n in c.most_common(30)))
+    loop_classes(body)
     # kernel-resource-usage remarks of this kernel (VGPRs, SGPRs, spills, scratch, occupancy)
     lines = r.stderr.split("\n")
     for k, line in enumerate(lines):
@@ -72,6 +73,47 @@ def main():
                     res.append(re.sub(r".*remark: *", "", l2).split(" [-Rpass")[0].strip())
             print("  ".join(res))
             break
+
+
+# rocprofv3's SQ_INSTS_VALU_* classes (the PMC passes' valu_mix), by opcode; the rest is "OTHER"
+CLASSES = [("TRANS_F32", r"^v_(rcp|rsq|sqrt|exp|log|sin|cos)_(iflag_)?f32"), ("TRANS_F64", r"^v_(rcp|rsq|sqrt)_f64"),
+           ("FMA_F64", r"^v_(fma|fmac)_f64|^v_div_fmas_f64"), ("MUL_F64", r"^v_mul_f64"), ("ADD_F64", r"^v_add_f64"),
+           ("FMA_F32", r"^v_(fma|fmac|fmaak|fmamk|mad|mac|pk_fma|fma_mix)\w*_f32"), ("MUL_F32", r"^v_(pk_)?mul_f32"),
+           ("ADD_F32", r"^v_(pk_)?(add|sub|subrev)_f32"), ("CVT", r"^v_cvt_"), ("INT64", r"^v_(mad_u64_u32|lshl_add_u64|\w+_u64|\w+_i64)"),
+           ("INT32", r"^v_(add|sub|subrev|mul_lo|mul_hi|mad_u32|mad_i32|lshl|lshr|ashr|and|or|xor|not|bfe|bfi|alignbit|"
+                     r"bitop3|perm|add3|lshl_add|lshl_or|and_or|or3|xad|min_u32|max_u32|min_i32|max_i32|bcnt|mbcnt)\w*")]
+
+
+def loop_classes(body):
+    """Static VALU mix of the kernel's outermost loop (first `Loop Header: Depth=1` block to its last
+    back-edge), in rocprofv3's SQ_INSTS_VALU_* classes, with OTHER broken down by opcode: what the
+    profile's valu_mix OTHER share is made of (compares, selects, moves, min/max, lane moves)."""
+    lines = body.split("\n")
+    best = None
+    for head, l in enumerate(lines):  # the largest outermost loop (the staging loops before it are small)
+        if "Loop Header: Depth=1" not in l:
+            continue
+        label = l.split(":")[0].strip()
+        tail = max((i for i, x in enumerate(lines) if re.search(r"s_(c)?branch\w*\s+" + re.escape(label) + r"\b", x)),
+                   default=None)
+        if tail is not None and tail > head and (best is None or tail - head > best[1] - best[0]):
+            best = (head, tail)
+    if best is None:
+        return
+    head, tail = best
+    ops = [l.strip().split()[0] for l in lines[head:tail + 1]
+           if l.strip() and not l.strip().startswith((".", ";")) and not l.strip().endswith(":")]
+    valu = [o for o in ops if o.startswith("v_")]
+    cls = collections.Counter()
+    other = collections.Counter()
+    for o in valu:
+        k = next((name for name, rx in CLASSES if re.match(rx, o)), "OTHER")
+        cls[k] += 1
+        if k == "OTHER":
+            other[re.sub(r"_e(32|64)$", "", o)] += 1
+    print(f"outer loop (lines {head}-{tail}): {len(ops)} instructions, {len(valu)} VALU")
+    print("  classes: " + "  ".join(f"{k} {n} ({n / len(valu):.0%})" for k, n in cls.most_common()))
+    print("  OTHER:   " + "  ".join(f"{k} {n}" for k, n in other.most_common(16)))
 
 
 if __name__ == "__main__":

@@ -21,6 +21,11 @@ def main():
     ap.add_argument("--ubench", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                      "profiles", "r02_ubench_valu_cost.jsonl"),
                     help="scripts/ubench/valu_cost output: per-class issue cost at 8 waves per SIMD")
+    ap.add_argument("--period-ns", type=float, default=None,
+                    help="the kernel's steady period from the same command's trace (scripts/trace_period.py): the "
+                         "time base of clock_mhz.  rocprofv3 --stats AverageNs is no time base with frames in flight "
+                         "(a dispatch's begin..end spans its wait behind the ones ahead), so without it no clock is "
+                         "reported")
     a = ap.parse_args()
     out = {}
     st = glob.glob(os.path.join(a.dir, "trace", "**", "*kernel_stats.csv"), recursive=True)
@@ -58,8 +63,11 @@ def main():
         # (MI355X_MICROARCH.md per-instruction constants, v_fma_f32), 1024 SIMDs.  Quarter-rate
         # and transcendental instructions hold the SIMD longer, so this is the issue fraction
         # counted in full-rate slots: a lower bound on how busy the vector pipe was.
-        clk = per["GRBM_GUI_ACTIVE"] / 8.0
-        out["clock_mhz"] = clk / (out["avg_ns"] * 1e-9) / 1e6 if out.get("avg_ns") else None
+        clk = per["GRBM_GUI_ACTIVE"] / 8.0  # busy cycles of one XCD per dispatch (PMC passes serialise dispatches)
+        out["xcd_busy_cycles"] = clk
+        if a.period_ns:
+            out["clock_mhz"] = clk / (a.period_ns * 1e-9) / 1e6
+            out["clock_basis"] = "GRBM_GUI_ACTIVE / 8 over the trace's steady period (--period-ns)"
         out["valu_issue_frac"] = per["SQ_INSTS_VALU"] * 2.0 / (1024.0 * clk)
     if "SQ_WAIT_INST_ANY" in per and per.get("SQ_WAVE_CYCLES"):
         out["wait_inst_frac"] = per["SQ_WAIT_INST_ANY"] / per["SQ_WAVE_CYCLES"]
@@ -80,7 +88,7 @@ def main():
                "SQ_INSTS_VALU_CVT": "v_cvt_f32_u32", "SQ_INSTS_VALU_FMA_F64": "v_fma_f64",
                "SQ_INSTS_VALU_ADD_F64": "v_mul_f64", "SQ_INSTS_VALU_MUL_F64": "v_mul_f64",
                "SQ_INSTS_VALU_TRANS_F64": "v_exp_f32"}
-    if os.path.exists(a.ubench) and out.get("clock_mhz") and "SQ_INSTS_VALU_FMA_F32" in per and "SQ_INSTS_VALU" in per:
+    if os.path.exists(a.ubench) and out.get("xcd_busy_cycles") and "SQ_INSTS_VALU_FMA_F32" in per and "SQ_INSTS_VALU" in per:
         cyc = {}
         for line in open(a.ubench):
             d = json.loads(line)
@@ -98,7 +106,7 @@ def main():
             other = max(per["SQ_INSTS_VALU"] - known, 0.0)
             busy += other * cyc["v_add_f32"]
             mix["OTHER"] = other / per["SQ_INSTS_VALU"]
-            simd_cycles = 1024.0 * out["clock_mhz"] * 1e6 * out["avg_ns"] * 1e-9
+            simd_cycles = 1024.0 * out["xcd_busy_cycles"]  # (no time base needed: cycles, not seconds)
             out["valu_mix"] = mix
             out["valu_cycles_per_inst_est"] = busy / per["SQ_INSTS_VALU"]
             out["valu_busy_est"] = busy / simd_cycles

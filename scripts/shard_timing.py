@@ -36,10 +36,16 @@ pstreams = [stream] + [torch.cuda.Stream(device="cuda:0") for _ in range(NSTREAM
 res, resq, resp = {}, {}, {}
 K = int(os.environ.get("SHARD_K", "8"))  # launches per pipelined measurement (the last one's tail is not overlapped)
 ns = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1, 2, 4, 8]
+# one-shot launches (shard_ms, shard_ms_queued) group their pixels as nrt_render does (16 Philox groups per
+# resident wave, api.cpp ONE_SHOT_GROUPS_PER_WAVE), pipelined ones as nrt_render_device does (4): the env knob
+# stands in for the API's choice here, unless the caller fixed it
+GPW_FIXED = os.environ.get("NRT_GROUPS_PER_WAVE")
 for n in ns:
     rows = (H + n - 1) // n
     launch = lambda: s.render_device(buf.data_ptr(), rows * W * 3, row_offset=0, row_stride=n,
                                      stream=stream.cuda_stream)
+    if not GPW_FIXED:
+        os.environ["NRT_GROUPS_PER_WAVE"] = "16"
     times, queued = [], []
     for it in range(4):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -60,6 +66,8 @@ for n in ns:
     res[n] = sum(times) / len(times)
     resq[n] = sum(queued) / len(queued)
     piped = []
+    if not GPW_FIXED:
+        os.environ.pop("NRT_GROUPS_PER_WAVE", None)
     for it in range(3):
         torch.cuda.synchronize()
         p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -84,4 +92,5 @@ out = {f"N={n}": {"shard_ms": round(t, 3), "efficiency_vs_N1": round(base / (n *
                   "efficiency_pipelined_vs_unpipelined_N1": round(base / (n * resp[n]), 4)}
        for n, t in res.items()}
 out["env"] = {k: v for k, v in os.environ.items() if k.startswith(("NRT_", "SHARD_"))}
+out["groups_per_wave"] = {"one_shot": GPW_FIXED or "16 (nrt_render)", "pipelined": GPW_FIXED or "4 (nrt_render_device)"}
 print(json.dumps(out))
