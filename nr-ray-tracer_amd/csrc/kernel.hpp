@@ -2823,7 +2823,10 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 #define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
 #endif
 #ifndef NRT_GRAB_FLAT
-#define NRT_GRAB_FLAT 2  // ... for the solid-colour (KF_FLAT) kernels: C5 9.91 -> 9.86 ms, C4 29.82 -> 29.64 ms
+// ... for the solid-colour (KF_FLAT) world-BVH kernels: C4 29.82 -> 29.64 ms (round 5); the world-list
+// ones (C5) take one again (round 6, same box: 9.78-9.81 against 9.82-9.85 ms with two, and a lone
+// launch's last groups end together: row shards at N = 8 unpipelined 0.838 -> 0.873 of linear)
+#define NRT_GRAB_FLAT 2
                          // (4 alternating runs; the textured earth: 5.14 -> 5.27 ms with 2, so it keeps 1)
 #endif
 #ifndef NRT_PROBE_HEAD
@@ -3480,7 +3483,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // with two slots one long path of the previous group starves the wave's lanes
         // (world BVH: long and short paths mix), so the BVH modes keep four.
         constexpr uint32_t NS = philox_slots<MAXD>();
-        constexpr uint32_t GRAB = FLAT ? (uint32_t)NRT_GRAB_FLAT : (uint32_t)NRT_GRAB;  // groups per queue atomic
+        constexpr uint32_t GRAB = FLAT && MAXD < 0 ? (uint32_t)NRT_GRAB_FLAT : (uint32_t)NRT_GRAB;  // groups per queue atomic
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
         const uint32_t GS = P * p.spp;  // samples per group (host: < 2^32)
