@@ -44,9 +44,17 @@ def main():
             print(f"skip {v}: no kernel stats")
             continue
         shutil.copy(stats, os.path.join(prof, f"{a.name}_{v}_kernel_stats.csv"))
+        tp = os.path.join(src, "trace_period.json")  # scripts/trace_period.py (pipelined runs)
+        if not os.path.exists(tp):
+            subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "trace_period.py"), os.path.join(src, "trace"),
+                            "--json", tp], check=False, capture_output=True)
+        period = None
+        if os.path.exists(tp):
+            with open(tp) as fh:
+                period = next(iter(json.load(fh).values()), {}).get("steady_period_ns")
         pmc_json = os.path.join(prof, f"{a.name}_{v}_pmc.json")
-        subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), src, "--json", pmc_json],
-                       check=True, capture_output=True)
+        subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), src, "--json", pmc_json] +
+                       (["--period-ns", str(period)] if period else []), check=True, capture_output=True)
         with open(pmc_json) as fh:
             d = json.load(fh)
         with open(os.path.join(src, "bench_trace.json")) as fh:
@@ -56,7 +64,6 @@ def main():
         e["variant"] = v
         e.update({k: d.get(k) for k in KEEP})
         e["bench_kernel_ms"] = bench["roofline"]["kernel_ms"]
-        tp = os.path.join(src, "trace_period.json")  # scripts/trace_period.py (pipelined runs)
         if os.path.exists(tp):
             shutil.copy(tp, os.path.join(prof, f"{a.name}_{v}_trace_period.json"))
             with open(tp) as fh:
