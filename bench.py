@@ -579,7 +579,11 @@ def run_ranks(args):
     # D = --pipeline row buffers rendered on D streams (D = 1: one stream); N = 1: the row buffers are
     # the frames; N > 1: rank 0 gathers into D frames.  Pinned host frames, one per buffer.
     D = max(1, args.pipeline if args.pipeline is not None else (3 if world == 1 else 2))
-    NB = max(2, D)  # buffers: at least two, so frame k's host copy overlaps frame k+1's render
+    # buffers: at least two, so frame k's host copy overlaps frame k+1's render; N > 1: one more than the
+    # render streams, so frame k + D's render waits for frame k - 1's gather, not frame k's: the gather's
+    # RCCL kernel finds CU slots only where a later render's persistent workgroups leave (its tail), and
+    # with D buffers render k + D would wait for exactly that
+    NB = max(2, D) if world == 1 else D + 1
     rbuf = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device=dev) for _ in range(NB)]
     # (N = 1: the current stream is one of them, so D = 3 render streams and the copy stream stay within
     # the process's 4 hardware queues; N > 1: it carries the gathers)

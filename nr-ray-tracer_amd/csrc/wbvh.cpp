@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
@@ -46,7 +47,7 @@ struct Builder {
     double pad = 0.0;
     uint32_t leaf_max = WBVH_LEAF_MAX;
 
-    static constexpr int BINS = 16;
+    int BINS = 16;  // SAH bins per axis (NRT_WBVH_BINS, 2..256)
 
     float down(double x) const {
         float f = (float)(x - pad);
@@ -84,9 +85,9 @@ struct Builder {
         for (int a = 0; a < 3; ++a) {
             const double ext = cb.hi[a] - cb.lo[a];
             if (!(ext > 0.0)) continue;
-            Box bin_box[BINS];
-            size_t bin_n[BINS] = {};
-            double bin_c[BINS] = {};
+            std::vector<Box> bin_box((size_t)BINS);
+            std::vector<size_t> bin_n((size_t)BINS, 0);
+            std::vector<double> bin_c((size_t)BINS, 0.0);
             const double scale = BINS / ext;
             for (size_t i = b; i < e; ++i) {
                 int k = (int)((items[i].c[a] - cb.lo[a]) * scale);
@@ -95,8 +96,8 @@ struct Builder {
                 ++bin_n[k];
                 bin_c[k] += items[i].cost;
             }
-            double right_area[BINS], right_c[BINS];
-            size_t right_n[BINS];
+            std::vector<double> right_area((size_t)BINS), right_c((size_t)BINS);
+            std::vector<size_t> right_n((size_t)BINS);
             Box acc;
             size_t cnt = 0;
             double csum = 0;
@@ -159,8 +160,13 @@ struct Builder {
     }
 };
 
-// Collapse the binary tree into 4-wide nodes: a 4-node's children are the
-// binary node's children with inner ones opened (largest box first) until four.
+// Collapse the binary tree into 4-wide nodes.  Greedy (the round-2 default): a 4-node's children are
+// the binary node's children with inner ones opened (largest box first) until four.  SAH (NRT_WBVH_COLLAPSE
+// = 1): the cover of every 4-node is chosen by dynamic programming over the binary tree to minimise the
+// expected cost (surface area heuristic: a node visit costs `visit` per unit of its box's area, a leaf its
+// primitives' costs), and a subtree of at most `leaf_max` primitives may become one leaf (its primitives
+// are contiguous in the binary tree's order) -- Ylitie, Karras & Laine, "Efficient incoherent ray
+// traversal on GPUs through compressed wide BVHs", HPG 2017, section 4.1, for a 4-wide tree.
 struct Collapse {
     const std::vector<DBvhNode>& n2;
     std::vector<DBvh4Node>& n4;
@@ -196,7 +202,114 @@ struct Collapse {
         int32_t child[4];
         for (int k = 0; k < 4; ++k)
             child[k] = k < (int)kids.size() ? (kids[k].ref >= 0 ? build(kids[k].ref) : kids[k].ref) : WBVH_DONE;
-        DBvh4Node& nd = n4[idx];
+        quantize(idx, kids, child);
+        return idx;
+    }
+
+    // ---- SAH collapse (dynamic programming)
+    double visit = 1.0;        // cost of a 4-node visit per unit area
+    uint32_t leaf_max = 4;     // a subtree of at most this many primitives may become a leaf
+    const std::vector<float>* prim_cost = nullptr;  // per BVH slot (binary order)
+    struct Info {
+        Slot box;
+        uint32_t first = 0, count = 0;  // the subtree's primitive slots in the binary order
+        double cost_sum = 0;            // its primitives' costs
+        double F[5] = {0, 0, 0, 0, 0};  // F[k]: best cover of the subtree with at most k slots
+        int8_t split[5] = {0, 0, 0, 0, 0};  // k >= 2: slots given to the left child (0: one slot)
+        bool as_leaf = false;           // F[1] is a leaf (else a 4-node / the binary leaf)
+        int8_t root_split = 0;          // the 4-node's slots to the left child
+    };
+    std::vector<Info> inner;               // per inner binary node
+    std::vector<Info> leaves;              // per binary leaf (index by order)
+    std::vector<int32_t> leaf_of_ref;      // (unused by value; leaves are keyed by their first slot)
+
+    Info& info(int32_t ref) {
+        if (ref >= 0) return inner[(size_t)ref];
+        const uint32_t v = ~(uint32_t)ref;
+        return leaves[v >> 3];
+    }
+    void prepare(int32_t ref, const Slot& box) {
+        Info& in = info(ref);
+        in.box = box;
+        if (ref < 0) {
+            const uint32_t v = ~(uint32_t)ref;
+            in.first = v >> 3;
+            in.count = (v & 7u) + 1u;
+            in.cost_sum = 0;
+            for (uint32_t k = 0; k < in.count; ++k) in.cost_sum += (*prim_cost)[in.first + k];
+            const double c = area(box) * in.cost_sum;
+            for (int k = 0; k <= 4; ++k) in.F[k] = c;
+            in.as_leaf = true;
+            return;
+        }
+        const DBvhNode& b = n2[(size_t)ref];
+        const Slot l{b.c0, {b.lo0[0], b.lo0[1], b.lo0[2]}, {b.hi0[0], b.hi0[1], b.hi0[2]}};
+        const Slot r{b.c1, {b.lo1[0], b.lo1[1], b.lo1[2]}, {b.hi1[0], b.hi1[1], b.hi1[2]}};
+        prepare(b.c0, l);
+        prepare(b.c1, r);
+        const Info &L = info(b.c0), &R = info(b.c1);
+        in.first = L.first;
+        in.count = L.count + R.count;
+        in.cost_sum = L.cost_sum + R.cost_sum;
+        // as a 4-node: its own visit plus the best 4-slot cover of its two children
+        double g = INFINITY;
+        for (int j = 1; j <= 3; ++j) {
+            const double c = L.F[j] + R.F[4 - j];
+            if (c < g) {
+                g = c;
+                in.root_split = (int8_t)j;
+            }
+        }
+        g += visit * area(box);
+        const bool can_leaf = in.count <= leaf_max && L.first + L.count == R.first;
+        const double lf = can_leaf ? area(box) * in.cost_sum : INFINITY;
+        in.as_leaf = lf < g;
+        in.F[1] = std::min(g, lf);
+        in.split[1] = 0;
+        for (int k = 2; k <= 4; ++k) {
+            in.F[k] = in.F[1];
+            in.split[k] = 0;
+            for (int j = 1; j < k; ++j) {
+                const double c = L.F[j] + R.F[k - j];
+                if (c < in.F[k]) {
+                    in.F[k] = c;
+                    in.split[k] = (int8_t)j;
+                }
+            }
+        }
+    }
+    // the cover items of `ref` with at most k slots
+    void cover(int32_t ref, int k, std::vector<Slot>& out) {
+        Info& in = info(ref);
+        if (ref < 0 || k == 1 || in.split[k] == 0) {
+            Slot s = in.box;
+            if (ref >= 0 && in.as_leaf) s.ref = ~(int32_t)((in.first << 3) | (in.count - 1u));
+            else s.ref = ref;
+            out.push_back(s);
+            return;
+        }
+        const DBvhNode& b = n2[(size_t)ref];
+        cover(b.c0, in.split[k], out);
+        cover(b.c1, k - in.split[k], out);
+    }
+    int32_t build_sah(int32_t ref) {  // ref: an inner binary node that is a 4-node
+        Info& in = info(ref);
+        const DBvhNode& b = n2[(size_t)ref];
+        std::vector<Slot> kids;
+        cover(b.c0, in.root_split, kids);
+        cover(b.c1, 4 - in.root_split, kids);
+        const int32_t idx = (int32_t)n4.size();
+        n4.emplace_back();
+        int32_t child[4];
+        for (int k = 0; k < 4; ++k)
+            child[k] = k < (int)kids.size() ? (kids[k].ref >= 0 ? build_sah(kids[k].ref) : kids[k].ref) : WBVH_DONE;
+        quantize(idx, kids, child);
+        return idx;
+    }
+
+    // node idx: quantized boxes of `kids`, child refs
+    void quantize(int32_t idx, const std::vector<Slot>& kids, const int32_t child[4]) {
+        DBvh4Node& nd = n4[(size_t)idx];
         std::memset(&nd, 0, sizeof nd);
         for (int a = 0; a < 3; ++a) {
             float lo = INFINITY, hi = -INFINITY;
@@ -232,7 +345,6 @@ struct Collapse {
             }
         }
         for (int k = 0; k < 4; ++k) nd.child[k] = child[k];
-        return idx;
     }
 };
 
@@ -320,6 +432,10 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
                          uint32_t leaf_max) {
     Builder bld;
     bld.leaf_max = std::max<uint32_t>(1u, std::min(leaf_max, WBVH_LEAF_MAX));
+    if (const char* e = std::getenv("NRT_WBVH_BINS")) {  // (A/B knob)
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 2 && v <= 256) bld.BINS = (int)v;
+    }
     bld.items.resize(bounds.size());
     double scale = 0.0;
     for (size_t i = 0; i < bounds.size(); ++i) {
@@ -340,7 +456,28 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
     if (bld.out.depth > WBVH_STACK) throw std::runtime_error("world BVH deeper than the kernel's stack");
     if (bld.out.root >= 0) {
         Collapse c{bld.out.nodes, bld.out.nodes4};
-        bld.out.root4 = c.build(bld.out.root);
+        const char* ce = std::getenv("NRT_WBVH_COLLAPSE");
+        if (ce && std::strtol(ce, nullptr, 10) == 1) {  // SAH collapse (A/B knob)
+            std::vector<float> slot_cost(bld.out.order.size());
+            for (size_t i = 0; i < slot_cost.size(); ++i) slot_cost[i] = bld.items.size() ? 1.0f : 1.0f;
+            for (size_t i = 0; i < slot_cost.size(); ++i)
+                slot_cost[i] = bld.out.order[i] < cost.size() ? cost[bld.out.order[i]] : 1.0f;
+            c.prim_cost = &slot_cost;
+            c.leaf_max = bld.leaf_max;
+            if (const char* v = std::getenv("NRT_WBVH_VISIT")) c.visit = std::strtod(v, nullptr);
+            c.inner.resize(bld.out.nodes.size());
+            c.leaves.resize(bld.out.order.size());
+            const DBvhNode& rb = bld.out.nodes[(size_t)bld.out.root];
+            Collapse::Slot root{bld.out.root, {}, {}};
+            for (int k = 0; k < 3; ++k) {
+                root.lo[k] = std::min(rb.lo0[k], rb.lo1[k]);
+                root.hi[k] = std::max(rb.hi0[k], rb.hi1[k]);
+            }
+            c.prepare(bld.out.root, root);
+            bld.out.root4 = c.build_sah(bld.out.root);
+        } else {
+            bld.out.root4 = c.build(bld.out.root);
+        }
         // nearest-first pushes all but one hit child: bound the stack along every path
         std::vector<uint32_t> need(bld.out.nodes4.size(), 0);
         for (size_t i = bld.out.nodes4.size(); i-- > 0;) {  // children have larger indices
