@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -474,6 +475,14 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
                 root.hi[k] = std::max(rb.hi0[k], rb.hi1[k]);
             }
             c.prepare(bld.out.root, root);
+            if (std::getenv("NRT_DEBUG_WBVH")) {
+                const Collapse::Info& ri = c.inner[(size_t)bld.out.root];
+                const Collapse::Info &L = c.info(rb.c0), &R = c.info(rb.c1);
+                std::fprintf(stderr, "nrt: SAH collapse objective %.3f (root split %d: %.3f + %.3f), root area %.4g\n",
+                             (L.F[ri.root_split] + R.F[4 - ri.root_split]) / Collapse::area(root) + c.visit,
+                             (int)ri.root_split, L.F[ri.root_split] / Collapse::area(root),
+                             R.F[4 - ri.root_split] / Collapse::area(root), (double)Collapse::area(root));
+            }
             bld.out.root4 = c.build_sah(bld.out.root);
         } else {
             bld.out.root4 = c.build(bld.out.root);
@@ -491,6 +500,46 @@ WorldBvh build_world_bvh(const std::vector<std::array<double, 6>>& bounds, const
             need[i] = (kids ? kids - 1 : 0) + deepest;
         }
         bld.out.stack4 = need[bld.out.root4];
+        if (std::getenv("NRT_DEBUG_WBVH")) {  // (diagnostics: the 4-wide tree's SAH cost, unit visit cost)
+            auto dec = [](const DBvh4Node& nd, int k, int a, float* lo, float* hi) {
+                const uint32_t ex = (nd.exps >> (10 * a)) & 1023u;
+                const float step = std::ldexp(1.0f + 0.25f * (float)(ex & 3u), (int)(ex >> 2) - 127);
+                *lo = nd.org[a] + (float)((nd.qlo[a] >> (8 * k)) & 255u) * step;
+                *hi = nd.org[a] + (float)((nd.qhi[a] >> (8 * k)) & 255u) * step;
+            };
+            double visits = 0, tests = 0, root_area = 0;
+            float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            size_t leaves = 0, leaf_prims = 0;
+            std::vector<double> node_area(bld.out.nodes4.size(), 0.0);
+            for (size_t i = 0; i < bld.out.nodes4.size(); ++i) {
+                const DBvh4Node& nd = bld.out.nodes4[i];
+                for (int k = 0; k < 4; ++k) {
+                    if (nd.child[k] == WBVH_DONE) continue;
+                    float lo[3], hi[3];
+                    for (int a = 0; a < 3; ++a) dec(nd, k, a, &lo[a], &hi[a]);
+                    const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2], ar = x * y + y * z + z * x;
+                    if (i == (size_t)bld.out.root4)
+                        for (int a = 0; a < 3; ++a) { rlo[a] = std::min(rlo[a], lo[a]); rhi[a] = std::max(rhi[a], hi[a]); }
+                    if (nd.child[k] >= 0) {
+                        node_area[(size_t)nd.child[k]] = ar;
+                    } else {
+                        const uint32_t v = ~(uint32_t)nd.child[k], cnt = (v & 7u) + 1u;
+                        ++leaves;
+                        leaf_prims += cnt;
+                        tests += ar * cnt;
+                    }
+                }
+            }
+            {
+                const double x = rhi[0] - rlo[0], y = rhi[1] - rlo[1], z = rhi[2] - rlo[2];
+                root_area = x * y + y * z + z * x;
+            }
+            for (size_t i = 0; i < node_area.size(); ++i) visits += i == (size_t)bld.out.root4 ? root_area : node_area[i];
+            std::fprintf(stderr, "nrt: world BVH %zu prims: %zu 4-nodes, %zu leaves (%zu prim slots), per ray ~%.2f visits "
+                                 "+ %.2f prim tests (SAH, root area = 1), stack %u\n",
+                         bld.out.order.size(), bld.out.nodes4.size(), leaves, leaf_prims, visits / root_area,
+                         tests / root_area, bld.out.stack4);
+        }
         if (need[bld.out.root4] > WBVH_STACK) {  // too deep for 4-wide traversal: binary only
             bld.out.nodes4.clear();
             bld.out.root4 = WBVH_DONE;
