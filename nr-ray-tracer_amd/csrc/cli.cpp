@@ -322,7 +322,14 @@ int main(int argc, char** argv) {
     const auto ti = std::chrono::steady_clock::now();
     int ndev = nrt_device_count();
     if (gpus < 1) gpus = 1;
-    if (gpus > ndev) die("requested " + std::to_string(gpus) + " GPUs, " + std::to_string(ndev) + " visible");
+    // (tests: NRT_MULTI_LOOPBACK=1 puts the N shards on device 0, csrc/multi.hip; NRT_CLI_SHARDS=1 takes the
+    // per-device row-shard threads below, as without RCCL)
+    const char* lb = getenv("NRT_MULTI_LOOPBACK");
+    const bool loopback = lb && *lb && strcmp(lb, "0") != 0;
+    const char* fs = getenv("NRT_CLI_SHARDS");
+    const bool force_shards = fs && strcmp(fs, "1") == 0;
+    if (gpus > ndev && !loopback) die("requested " + std::to_string(gpus) + " GPUs, " + std::to_string(ndev) + " visible");
+    auto dev_of = [&](int g) { return loopback ? 0 : g; };
     // --gpus N > 1: the library's multi-GPU render (nrt_render_opts.gpus): rows interleaved over
     // devices 0 .. N-1, one RCCL gather to device 0, un-permuted there; without a usable
     // librccl (nrt_render_prepare: NRT_E_UNSUPPORTED) one host thread per device renders its row shard
@@ -330,13 +337,13 @@ int main(int argc, char** argv) {
     bool shards = false;
     if (gpus > 1) {
         opts.gpus = (uint32_t)gpus;
-        const int rc = nrt_render_prepare(sc, &cam, &opts);
+        const int rc = force_shards ? NRT_E_UNSUPPORTED : nrt_render_prepare(sc, &cam, &opts);
         if (rc == NRT_E_UNSUPPORTED) {
             if (verbose) fprintf(stderr, " multi-GPU render without RCCL (%s): per-device row shards\n", nrt_last_error());
             opts.gpus = 0;
             shards = true;
             for (int g = 0; g < gpus; ++g)
-                if (nrt_scene_upload(sc, g) != NRT_OK) die(nrt_last_error());
+                if (nrt_scene_upload(sc, dev_of(g)) != NRT_OK) die(nrt_last_error());
         } else if (rc != NRT_OK) {
             die(nrt_last_error());
         }
@@ -352,7 +359,7 @@ int main(int argc, char** argv) {
         for (int g = 0; g < gpus; ++g)
             th.emplace_back([&, g]() {
                 nrt_render_opts o = opts;
-                o.device = g;
+                o.device = dev_of(g);
                 o.row_offset = (uint32_t)g;
                 o.row_stride = (uint32_t)gpus;
                 part[(size_t)g].resize((size_t)nrt_rows_selected(H, &o) * W * 3);

@@ -19,11 +19,12 @@ CLI = os.path.join(os.path.dirname(nrt.LIB_PATH), "nrt-cli")
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def run(args, tmp_path):
+def run(args, tmp_path, extra_env=None):
     env = dict(os.environ)
     for k in list(env):
         if k.startswith("NR_RT_CAMERA_"):
             del env[k]
+    env.update(extra_env or {})
     return subprocess.run([CLI, "render", *args], cwd=GOLDEN, capture_output=True, text=True, env=env, timeout=300)
 
 
@@ -88,3 +89,24 @@ def test_cli_multi_gpu_rows_equal_single_gpu(tmp_path):
         assert r.returncode == 0, r.stderr
         outs.append(read_pfm(out))
     np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision,rng", [("f32", "philox"), ("f64", "chacha8")])
+def test_cli_multi_gpu_code_on_one_gpu(tmp_path, precision, rng):
+    """`--gpus 3` on one GPU: the library's N-GPU render through the test-only loopback (NRT_MULTI_LOOPBACK=1:
+    the three shards on device 0, the gather as device copies, csrc/multi.hip), and the CLI's own fallback
+    for a host without a usable librccl (NRT_CLI_SHARDS=1: one thread per shard, rows y = g (mod 3), the
+    frame un-permuted on the host, as nrt_render_prepare's NRT_E_UNSUPPORTED makes it): both PFMs equal the
+    one-GPU render bit for bit."""
+    args = ["scenes/cornell-box-scene.json", "-W", "40", "-H", "29", "--samples-per-pixel", "4", "--precision",
+            precision, "--rng", rng, "-f"]
+    outs = []
+    for name, gpus, env in (("one", 1, {}), ("loop", 3, {"NRT_MULTI_LOOPBACK": "1"}),
+                            ("shards", 3, {"NRT_MULTI_LOOPBACK": "1", "NRT_CLI_SHARDS": "1"})):
+        out = tmp_path / f"{name}.pfm"
+        r = run(args + ["--gpus", str(gpus), "-o", str(out)], tmp_path, env)
+        assert r.returncode == 0, (name, r.stderr)
+        outs.append(read_pfm(out))
+    np.testing.assert_array_equal(outs[1].view(np.uint32), outs[0].view(np.uint32))
+    np.testing.assert_array_equal(outs[2].view(np.uint32), outs[0].view(np.uint32))

@@ -269,3 +269,21 @@ def test_library_multi_gpu_prepare_and_stream_checks(monkeypatch):
         o = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
         with pytest.raises(nrt.NrtError, match="belongs to device 1"):
             s.render_device(o.data_ptr(), o.numel(), device=0, stream=other.cuda_stream, gpus=1)
+
+
+@pytest.mark.parametrize("scene,precision,rng", [
+    ("scenes/utah-teapot-scene.json", "f32", "philox"),   # world BVH, scene-specialised (BvhSig)
+    ("scenes/utah-teapot-scene.json", "f64", "chacha8"),  # the exact kernel's persistent walk, LDS stack
+    ("scenes/earth.toml", "f32", "philox"),               # PAL16 textures (KF_TEXPAL), f32 spheres
+    ("scenes/spheres.toml", "f64", "chacha8"),            # the unfiltered exact walk (XWalkU)
+])
+def test_library_multi_gpu_loopback_other_kernels(monkeypatch, scene, precision, rng):
+    """The N-GPU render's shards go through every kernel family (loopback, N = 3 and 8, a height that leaves
+    short shards): bit-identical to the single-device render."""
+    monkeypatch.setenv("NRT_MULTI_LOOPBACK", "1")
+    with in_golden():
+        s = nrt.Scene.load(scene, nrt.CameraConfig(width=40, height=27, samples_per_pixel=4))
+    want = s.render(precision=precision, rng=rng, device=0)
+    for g in (3, 8):
+        np.testing.assert_array_equal(s.render(precision=precision, rng=rng, device=0, gpus=g), want,
+                                      err_msg=f"gpus={g}")
