@@ -2855,10 +2855,13 @@ __host__ __device__ constexpr uint32_t philox_pool_bytes(uint32_t P) {
 template <typename R, class G, int MAXD, class SIG = NoSig>
 constexpr int min_waves_per_simd(int kflags = 0) {
 #ifndef NRT_WORLD_LIST_WAVES
-#define NRT_WORLD_LIST_WAVES 6
+#define NRT_WORLD_LIST_WAVES 6  // the generic world-list loop (NoSig)
+#endif
+#ifndef NRT_JIT_LIST_WAVES
+#define NRT_JIT_LIST_WAVES 7  // scene-specialised world lists with textures (the earth: 72 VGPRs; C3 5.135 -> 5.052 ms)
 #endif
 #ifndef NRT_FLAT_WAVES
-#define NRT_FLAT_WAVES NRT_WORLD_LIST_WAVES
+#define NRT_FLAT_WAVES 8  // scene-specialised solid-colour world lists (C5: 61 VGPRs; 9.777 -> 9.543 ms)
 #endif
 #ifndef NRT_F64_WAVES
 #define NRT_F64_WAVES 4  // f64 kernels, plane-only scenes (KF_PLANES): 4 waves per SIMD
@@ -2872,24 +2875,37 @@ constexpr int min_waves_per_simd(int kflags = 0) {
     if (sizeof(R) == 8 && SIG::lstack) return NRT_F64_LSTACK_WAVES;
     if (sizeof(R) == 8) return (kflags & KF_PLANES) ? NRT_F64_WAVES : NRT_F64_SPHERE_WAVES;
 #ifndef NRT_WBVH_WAVES
-#define NRT_WBVH_WAVES 6  // KF_FLAT world BVH (teapot): 80 VGPRs, no spill (5 at the compiler's 81: C4 33.84 -> 33.60 ms)
+#define NRT_WBVH_WAVES 6  // KF_FLAT world BVH, generic (NoSig): 80 VGPRs, no spill
+#endif
+#ifndef NRT_JIT_WBVH_WAVES
+#define NRT_JIT_WBVH_WAVES 7  // KF_FLAT world BVH, scene-specialised (BvhSig; the teapot: C4 30.02 -> 29.74 ms)
 #endif
 #ifndef NRT_WBVH_SPHERE_WAVES
 #define NRT_WBVH_SPHERE_WAVES 5  // world BVH with spheres / textures (not KF_FLAT): 96 VGPRs, 5 spilled (spheres 1080p 32.5 -> 31.3 ms)
 #endif
-    if (sizeof(R) == 4 && MAXD < 0 && !G::uses_lds) return (kflags & KF_FLAT) ? NRT_WBVH_WAVES : NRT_WBVH_SPHERE_WAVES;
-    if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT)) return NRT_FLAT_WAVES;
-    return (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN)) ? NRT_WORLD_LIST_WAVES : 1;
+    // The f32 Philox kernels at 7 or more waves per SIMD read the camera at its use (cam3 RELOAD): the
+    // SGPR budget shrinks with the wave count (7 waves: 94, 8: 78 here), and the 21 camera SGPRs held
+    // through the loop were spilled to VGPR lanes; the generic kernels (NoSig) keep their counts (at 7 / 8
+    // they spill to scratch).  Frames identical (the waves place no work, the same loads feed the same FMAs).
+    constexpr bool JIT = SIG::n > 0 || SIG::bvh != 0;
+    if (sizeof(R) == 4 && MAXD < 0 && !G::uses_lds)
+        return (kflags & KF_FLAT) ? (JIT ? NRT_JIT_WBVH_WAVES : NRT_WBVH_WAVES) : NRT_WBVH_SPHERE_WAVES;
+    if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && (kflags & KF_FLAT) && JIT) return NRT_FLAT_WAVES;
+    if (sizeof(R) == 4 && MAXD == 0 && !G::uses_lds && !(kflags & KF_PERLIN))
+        return JIT ? NRT_JIT_LIST_WAVES : NRT_WORLD_LIST_WAVES;
+    return 1;
 }
 static_assert(BLOCK % 64 == 0, "stack / ring / accumulator layouts assume whole waves");
 
 // Camera vector q of RenderParams: the f32 kernel takes the host-rounded copy
 // (kernel arguments stay in SGPRs), the f64 kernel the double.
-template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
-    if constexpr (sizeof(R) == 4) {
-#if NRT_CAM_RELOAD
-        // scalar loads from the kernel arguments at the use (offset laundered: not hoisted), as the
-        // f64 branch below: 21 SGPRs less held through the loop (occupancy experiments)
+// RELOAD (f32): scalar loads from the kernel arguments at the use (offset laundered: not hoisted), as
+// the f64 branch below: 21 SGPRs less held through the loop.  The kernels at 7+ waves per SIMD take it
+// (min_waves_per_simd; C5 at 8 waves: 37 SGPRs spilled to VGPR lanes without it, 12 with it; at 6 / 7
+// waves with SGPRs to spare the reloads alone cost 1-1.5 %)
+template <typename R, bool RELOAD = NRT_CAM_RELOAD != 0>
+__device__ __forceinline__ V<R> cam3(const RenderParams& p, int q, const double* d) {
+    if constexpr (sizeof(R) == 4 && RELOAD) {
         (void)p;
         (void)d;
         uint32_t o = (uint32_t)__builtin_offsetof(RenderParams, camf) + (uint32_t)q * 12u;
@@ -2898,9 +2914,8 @@ template <typename R> __device__ __forceinline__ V<R> cam3(const RenderParams& p
         const KArgF base = (KArgF)__builtin_amdgcn_kernarg_segment_ptr();
         const __attribute__((address_space(4))) float* fp = (const __attribute__((address_space(4))) float*)(base + o);
         return mk(fp[0], fp[1], fp[2]);
-#else
+    } else if constexpr (sizeof(R) == 4) {
         return mk(p.camf[q][0], p.camf[q][1], p.camf[q][2]);
-#endif
     } else {
         // f64: scalar loads from the kernel arguments at the use (the offset laundered, so the loads
         // are not hoisted out of the loop): seven f64 vectors held live through the loop spilled the
@@ -2985,13 +3000,14 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
     if constexpr (LDS_SCENE) sc = stage_scene(gsc, lds + ring_bytes + acc_bytes + stack_bytes, wprim_lds_stride(MAXD));
 
     G g;
+    constexpr bool CAM_RELOAD = NRT_CAM_RELOAD || (sizeof(R) == 4 && min_waves_per_simd<R, G, MAXD, SIG>(KFLAGS) >= 7);
     // Camera vectors (camera.rs:205-227) q = 0..6: top_left, delta_u, delta_v, look_from,
     // disk_u, disk_v, background (f32: the host-rounded copies, kernel arguments in SGPRs)
     auto cam = [&](int q) -> V<R> {
         const double* d = q == 0 ? p.top_left : q == 1 ? p.pixel_delta_u : q == 2 ? p.pixel_delta_v
                         : q == 3 ? p.look_from : q == 4 ? p.defocus_disk_u : q == 5 ? p.defocus_disk_v
                         : p.background;
-        return cam3<R>(p, q, d);
+        return cam3<R, CAM_RELOAD>(p, q, d);
     };
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform values live in SGPRs
 

@@ -41,7 +41,7 @@ def main():
                      f"const nrt::DSceneView<{targs.split(',')[0].strip()}>);\n")
         frag = ""
     else:
-        frag = args.pop(0) if args and not args[0].startswith("-") else "PhiloxELi0ELb0ELb1ELi4EE"
+        frag = args.pop(0) if args and not args[0].startswith("-") else "PhiloxELi0ELb0ELb1ELi4ENS0_5NoSig"
         src = os.path.join(pkg, "csrc", "kernels_exact.hip" if exact else "kernels_fast.hip")
     out = os.path.join(td, "all.s")
     r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, *inc, src, "-o", out, *args], cwd=pkg, capture_output=True,
