@@ -1106,6 +1106,8 @@ struct WorldSig {
     static constexpr uint32_t n = sizeof...(RUNS);
     template <uint32_t KIND>
     static constexpr bool has() { return ((((RUNS & WRUN_KIND_MASK) == KIND) || ...)); }
+    // the list's units use the ray's 1/d (flatten.cpp's WFLAG_AXIS_QUADS, known at compile time)
+    static constexpr bool axis = ((((RUNS & WRUN_KIND_MASK) >= PRIM_QUAD_X && (RUNS & WRUN_KIND_MASK) != PRIM_SPHERE32)) || ...);
     static constexpr int bvh = 0;
     static constexpr bool tie = false;
     static constexpr int prims = 0;
@@ -1172,7 +1174,10 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
     const f32x2 dox = {ray.d.x, ray.o.x}, doy = {ray.d.y, ray.o.y}, doz = {ray.d.z, ray.o.z};
     float inv[3], oinv[3];  // axis-aligned quads and rooms: 1/d and o/d
     uint32_t entry_slot[3] = {0u, 2u, 4u};  // rooms: face slot 2*axis + side entered along each axis
-    if (sc.wflags & WFLAG_AXIS_QUADS) {
+    bool axis;
+    if constexpr (SIG::n > 0) axis = SIG::axis;  // (no uniform flag held through the loop)
+    else axis = (sc.wflags & WFLAG_AXIS_QUADS) != 0u;
+    if (axis) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             inv[a] = __builtin_amdgcn_rcpf((&ray.d.x)[a]);
