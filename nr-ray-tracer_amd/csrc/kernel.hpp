@@ -2828,11 +2828,11 @@ __device__ __forceinline__ DSceneView<R> stage_scene(const DSceneView<R>& g, uns
 #define NRT_GRAB 1  // Philox groups per queue atomic (render_kernel's fetch)
 #endif
 #ifndef NRT_GRAB_FLAT
-// ... for the solid-colour (KF_FLAT) world-BVH kernels: C4 29.82 -> 29.64 ms (round 5); the world-list
-// ones (C5) take one again (round 6, same box: 9.78-9.81 against 9.82-9.85 ms with two, and a lone
-// launch's last groups end together: row shards at N = 8 unpipelined 0.838 -> 0.873 of linear)
-#define NRT_GRAB_FLAT 2
-                         // (4 alternating runs; the textured earth: 5.14 -> 5.27 ms with 2, so it keeps 1)
+// ... for the solid-colour (KF_FLAT) world-BVH kernels: two measured C4 29.82 -> 29.64 ms at 6 waves per
+// SIMD (round 5), but at 7 one is faster again (29.69 -> 29.47 ms, three alternating runs); the world
+// lists (C5) take one too (9.78-9.81 against 9.82-9.85 ms with two, and a lone launch's last groups end
+// together: row shards at N = 8 unpipelined 0.838 -> 0.873 of linear), the textured earth 5.14 vs 5.27
+#define NRT_GRAB_FLAT 1
 #endif
 #ifndef NRT_PROBE_HEAD
 // 1: skip queue heads an agent-scope load shows empty before the atomic (saved C5 ~2 MB of HBM
