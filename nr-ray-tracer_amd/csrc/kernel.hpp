@@ -942,11 +942,14 @@ __device__ __forceinline__ BoxPlanes box_planes(ConstPrimWorld<float> q, const f
 // The face quad (0-5, the unit's record + 1 + face) through which the ray enters (entry) or leaves
 // the box: face slot 2*axis + side (side 0 = local plane x' = 0; entered there when d' > 0), the
 // quad that lies there from 3 bits per slot of meta.  sy: BOXY's y slot pair from the world ray.
+// 1 for a negative x, else 0: the sign bit (= x < 0 for every non-NaN x, -inf from rcp(-0) included; a
+// NaN ray's tests all fail, so its slots are never read): one shift instead of a compare and a select
+__device__ __forceinline__ uint32_t neg_bit(float x) { return __float_as_uint(x) >> 31; }
 __device__ __forceinline__ uint32_t box_face(const BoxPlanes& b, uint32_t meta, bool entry, uint32_t sy) {
     const float nx = fminf(b.ax, b.bx), ny = fminf(b.ay, b.by), nz = fminf(b.az, b.bz);
     const float fx = fmaxf(b.ax, b.bx), fy = fmaxf(b.ay, b.by), fz = fmaxf(b.az, b.bz);
     const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
-    const uint32_t sx = b.ix < 0.0f ? 1u : 0u, sz = b.iz < 0.0f ? 5u : 4u;
+    const uint32_t sx = neg_bit(b.ix), sz = 4u | neg_bit(b.iz);
     uint32_t se = sz, sxit = sz ^ 1u;
     se = tn == ny ? sy : se;
     se = tn == nx ? sx : se;
@@ -970,7 +973,7 @@ __device__ __forceinline__ int32_t resolve_box_face(ConstPrimWorld<float> wp, in
         face = box_face(boxy_planes(q, dox, doz, inv, oinv), q->meta, entry, entry_slot[1]);
     } else if (BOX) {
         const BoxPlanes b = box_planes(q, dox, doy, doz);
-        face = box_face(b, q->meta, entry, b.iy < 0.0f ? 3u : 2u);
+        face = box_face(b, q->meta, entry, 2u | neg_bit(b.iy));
     }
     return (int32_t)(k + 1u + face);
 }
@@ -1048,7 +1051,7 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
 #if NRT_BOX_DEFER
             best = ok ? (int32_t)(k | WBEST_BOX | (entry ? WBEST_ENTRY : 0u)) : best;
 #else
-            best = ok ? (int32_t)(k + 1 + box_face(bp, q->meta, entry, bp.iy < 0.0f ? 3u : 2u)) : best;
+            best = ok ? (int32_t)(k + 1 + box_face(bp, q->meta, entry, 2u | neg_bit(bp.iy))) : best;
 #endif
         }
         return;
@@ -1182,7 +1185,7 @@ __device__ __forceinline__ bool trace_world(const DSceneView<R>& sc, const Ray<R
         for (int a = 0; a < 3; ++a) {
             inv[a] = __builtin_amdgcn_rcpf((&ray.d.x)[a]);
             oinv[a] = (&ray.o.x)[a] * inv[a];
-            entry_slot[a] = 2u * a + (inv[a] < 0.0f ? 1u : 0u);  // d > 0 enters at the low plane
+            entry_slot[a] = 2u * a + neg_bit(inv[a]);  // d > 0 enters at the low plane
         }
     }
     uint32_t k = 0;
