@@ -52,6 +52,10 @@ constexpr int BLOCK = NRT_BLOCK;
                        // changed); a wave that has traced finishes its step first (C5 10.36 -> 10.28 ms,
                        // C4 33.50 -> 33.18, C2 0.927 -> 0.920, C3 +-0.2 %; frames identical)
 #endif
+#ifndef NRT_SETPRIO_TEX
+#define NRT_SETPRIO_TEX 0  // ... in the textured world lists (KF_TEXPAL, the earth) at 7 waves: 0 (never
+                           // changed) measured C3 5.063 -> 5.024 ms; 1: 5.061 (two alternating runs)
+#endif
 #ifndef NRT_WBVH_IFIF
 // world BVH: one node visit or one primitive per lane and trip (wbvh_trip) in the KF_FLAT
 // variant (triangles / quads only: a primitive costs a fifth of a visit; C4 6 307 -> 6 400
@@ -83,6 +87,14 @@ constexpr int BLOCK = NRT_BLOCK;
 #endif
 #ifndef NRT_WALK_CONTRACT
 #define NRT_WALK_CONTRACT 1  // FMA contraction in the exact kernel's f32 culling walk and prefilter
+#endif
+#ifndef NRT_PK_LIST
+#define NRT_PK_LIST 0  // axis quads and boxes turned about y: (d, o) pairs as packed f32 ops; 0: the same
+                       // expressions per component (the same roundings, frames identical): C5 9.310 -> 9.235 ms
+#endif
+#ifndef NRT_PK_QUAD
+#define NRT_PK_QUAD 1  // ... general quads / triangles and boxes (three-term rows): packed (quads.toml 1024^2
+                       // spp 64: 0.760 ms packed, 0.827 unpacked)
 #endif
 #ifndef NRT_BOX_DEFER
 // world list: 1 = a box unit's (PRIM_BOX / PRIM_BOXY) face is resolved once, for the winner of the whole
@@ -886,8 +898,13 @@ __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t
         const ConstPrimWorld<float> q = wp + k;
         const float t = __builtin_fmaf(q->N[A1], inv[A], -oinv[A]);  // (P - o_a) / d_a
         const float p1 = o[A1] + t * d[A1], p2 = o[A2] + t * d[A2];
+#if NRT_PK_LIST
         const f32x2 ab = f32x2{q->AB[2 * A1], q->AB[2 * A1 + 1]} * p1 + f32x2{q->AB[2 * A2], q->AB[2 * A2 + 1]} * p2 -
                          f32x2{q->AB[6], q->AB[7]};
+#else  // the same expressions per component (the same contraction: the same roundings)
+        const f32x2 ab = {q->AB[2 * A1] * p1 + q->AB[2 * A2] * p2 - q->AB[6],
+                          q->AB[2 * A1 + 1] * p1 + q->AB[2 * A2 + 1] * p2 - q->AB[7]};
+#endif
         const float lo = fminf(ab.x, ab.y);
         const bool ok = (fabsf(d[A]) >= q->N[A2]) & (t >= 0.001f) & (t <= t_best) & (lo >= 0.0f) & (ab.x <= 1.0f) &
                         (ab.y <= 1.0f);
@@ -907,8 +924,13 @@ struct BoxPlanes {
 __device__ __forceinline__ BoxPlanes boxy_planes(ConstPrimWorld<float> q, const f32x2& dox, const f32x2& doz,
                                                  const float inv[3], const float oinv[3]) {
     BoxPlanes b;
+#if NRT_PK_LIST
     const f32x2 la = dox * q->N[0] + doz * q->N[2];  // (row_A . d, row_A . o)
     const f32x2 lb = dox * q->AB[0] + doz * q->AB[2];
+#else
+    const f32x2 la = {dox.x * q->N[0] + doz.x * q->N[2], dox.y * q->N[0] + doz.y * q->N[2]};
+    const f32x2 lb = {dox.x * q->AB[0] + doz.x * q->AB[2], dox.y * q->AB[0] + doz.y * q->AB[2]};
+#endif
     b.ix = __builtin_amdgcn_rcpf(la.x);
     b.iz = __builtin_amdgcn_rcpf(lb.x);
     b.iy = 0.0f;
@@ -924,9 +946,17 @@ __device__ __forceinline__ BoxPlanes box_planes(ConstPrimWorld<float> q, const f
                                                 const f32x2& doz) {
     BoxPlanes b;
     // (d', E^-1 o) per local axis; x' = E^-1 x - E^-1 c
+#if NRT_PK_QUAD
     const f32x2 lx = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];
     const f32x2 ly = dox * q->AB[0] + doy * q->AB[1] + doz * q->AB[2];
     const f32x2 lz = dox * q->AB[4] + doy * q->AB[5] + doz * q->AB[6];
+#else
+    auto row = [&](float a, float b, float c) {
+        return f32x2{dox.x * a + doy.x * b + doz.x * c, dox.y * a + doy.y * b + doz.y * c};
+    };
+    const f32x2 lx = row(q->N[0], q->N[1], q->N[2]), ly = row(q->AB[0], q->AB[1], q->AB[2]),
+                lz = row(q->AB[4], q->AB[5], q->AB[6]);
+#endif
     b.ix = __builtin_amdgcn_rcpf(lx.x);
     b.iy = __builtin_amdgcn_rcpf(ly.x);
     b.iz = __builtin_amdgcn_rcpf(lz.x);
@@ -1077,11 +1107,21 @@ __device__ __forceinline__ void world_run(ConstPrimWorld<float> wp, uint32_t kin
     const bool quad = kind == PRIM_QUAD;
     for (; k < end; ++k) {
         const ConstPrimWorld<float> q = wp + k;
+#if NRT_PK_QUAD
         const f32x2 dn = dox * q->N[0] + doy * q->N[1] + doz * q->N[2];  // (N.d, N.o)
+#else
+        const f32x2 dn = {dox.x * q->N[0] + doy.x * q->N[1] + doz.x * q->N[2],
+                          dox.y * q->N[0] + doy.y * q->N[1] + doz.y * q->N[2]};  // (N.d, N.o)
+#endif
         const float t = (q->D - dn.y) * __builtin_amdgcn_rcpf(dn.x);
         const float px = ray.o.x + t * ray.d.x, py = ray.o.y + t * ray.d.y, pz = ray.o.z + t * ray.d.z;
+#if NRT_PK_QUAD
         const f32x2 ab = f32x2{q->AB[0], q->AB[1]} * px + f32x2{q->AB[2], q->AB[3]} * py +
                          f32x2{q->AB[4], q->AB[5]} * pz - f32x2{q->AB[6], q->AB[7]};  // (alpha, beta)
+#else
+        const f32x2 ab = {q->AB[0] * px + q->AB[2] * py + q->AB[4] * pz - q->AB[6],
+                          q->AB[1] * px + q->AB[3] * py + q->AB[5] * pz - q->AB[7]};  // (alpha, beta)
+#endif
         const float lo = fminf(ab.x, ab.y);
         // quad closed [0,1]^2 (plane.rs:121-126), triangle open (plane.rs:128-133); a NaN
         // coordinate can only come from a rejected denominator or t
@@ -3507,6 +3547,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
         // with two slots one long path of the previous group starves the wave's lanes
         // (world BVH: long and short paths mix), so the BVH modes keep four.
         constexpr uint32_t NS = philox_slots<MAXD>();
+        constexpr int SETPRIO = (KFLAGS & KF_TEXPAL) ? NRT_SETPRIO_TEX : NRT_SETPRIO;
         constexpr uint32_t GRAB = FLAT && MAXD < 0 ? (uint32_t)NRT_GRAB_FLAT : (uint32_t)NRT_GRAB;  // groups per queue atomic
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t P = p.wave_pixels, logP = p.wave_pixels_log2;
@@ -3661,7 +3702,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                 if (free) fetch(r);
             }
             if (exhausted && !ready && GS - next == 0u && __ballot(alive) == 0ull) break;
-            if constexpr (NRT_SETPRIO > 0) __builtin_amdgcn_s_setprio(0);
+            if constexpr (SETPRIO > 0) __builtin_amdgcn_s_setprio(0);
             const unsigned long long t0 = stamp();
             HitMin<R, MAXD> hm;
             bool hit = false, sh, traced;
@@ -3698,7 +3739,7 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
                                                                    p.exact_thread != 0);
             }
             const unsigned long long t1 = stamp();
-            if constexpr (NRT_SETPRIO > 0) __builtin_amdgcn_s_setprio(NRT_SETPRIO);  // shading at raised priority
+            if constexpr (SETPRIO > 0) __builtin_amdgcn_s_setprio(SETPRIO);  // shading at raised priority
             Rec<R> h;
             MatV<R> m;
             V<R> contrib;  // (set by surface() wherever it is read: ends implies sh)
