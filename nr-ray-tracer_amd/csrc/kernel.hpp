@@ -89,12 +89,12 @@ constexpr int BLOCK = NRT_BLOCK;
 #define NRT_WALK_CONTRACT 1  // FMA contraction in the exact kernel's f32 culling walk and prefilter
 #endif
 #ifndef NRT_PK_LIST
-#define NRT_PK_LIST 0  // axis quads and boxes turned about y: (d, o) pairs as packed f32 ops; 0: the same
-                       // expressions per component (the same roundings, frames identical): C5 9.310 -> 9.235 ms
+#define NRT_PK_LIST 0  // boxes turned about y: (d, o) pairs as packed f32 ops; 0: the same expressions per
+                       // component (the same roundings, frames identical): C5 9.310 -> 9.235 ms
 #endif
 #ifndef NRT_PK_QUAD
-#define NRT_PK_QUAD 1  // ... general quads / triangles and boxes (three-term rows): packed (quads.toml 1024^2
-                       // spp 64: 0.760 ms packed, 0.827 unpacked)
+#define NRT_PK_QUAD 1  // ... quads (axis and general), triangles and boxes: packed (quads.toml, five axis quads,
+                       // 1024^2 spp 64: 0.760 ms packed, 0.827 unpacked)
 #endif
 #ifndef NRT_BOX_DEFER
 // world list: 1 = a box unit's (PRIM_BOX / PRIM_BOXY) face is resolved once, for the winner of the whole
@@ -898,7 +898,7 @@ __device__ __forceinline__ void axis_quad_run(ConstPrimWorld<float> wp, uint32_t
         const ConstPrimWorld<float> q = wp + k;
         const float t = __builtin_fmaf(q->N[A1], inv[A], -oinv[A]);  // (P - o_a) / d_a
         const float p1 = o[A1] + t * d[A1], p2 = o[A2] + t * d[A2];
-#if NRT_PK_LIST
+#if NRT_PK_QUAD
         const f32x2 ab = f32x2{q->AB[2 * A1], q->AB[2 * A1 + 1]} * p1 + f32x2{q->AB[2 * A2], q->AB[2 * A2 + 1]} * p2 -
                          f32x2{q->AB[6], q->AB[7]};
 #else  // the same expressions per component (the same contraction: the same roundings)
