@@ -445,6 +445,9 @@ struct Philox {
 // 32-bit word -> uniform [0, 1) (f32: 23 bits, f64: 32 bits)
 template <typename R> __device__ __forceinline__ R u01(uint32_t w);
 template <> __device__ __forceinline__ float u01<float>(uint32_t w) { return __uint_as_float(0x3F800000u | (w >> 9)) - 1.0f; }
+// [1, 2) from the same 23 bits: u01<float> = u12 - 1 exactly, so an affine map of u01 folds its offset
+// into one op with the same rounding (2 u01 - 1 = 2 u12 - 3, 1 - u01 = 2 - u12, u01 - 0.5 = u12 - 1.5)
+__device__ __forceinline__ float u12(uint32_t w) { return __uint_as_float(0x3F800000u | (w >> 9)); }
 template <> __device__ __forceinline__ double u01<double>(uint32_t w) { return (double)w * 0x1p-32; }
 
 // rand 0.9 `random_range(low..high)` / `(low..=high)` on f64: one draw,
@@ -541,9 +544,9 @@ __device__ __forceinline__ V<R> rejection_wave(G& g, bool need) {
 // p uniform in the unit ball, p/|p|^2 = u/r with u uniform on the sphere and
 // r = U^(1/3); p uniform in the unit disk, p/|p|^2 = (cos t, sin t)/sqrt(U).
 template <typename R> __device__ __forceinline__ V<R> unit_ball_inverse(uint32_t w0, uint32_t w1, uint32_t w2) {
-    const R z = fmad(R(2), u01<R>(w0), R(-1));
+    const R z = sizeof(R) == 4 ? (R)__builtin_fmaf(2.0f, u12(w0), -3.0f) : fmad(R(2), u01<R>(w0), R(-1));
     const R turn = u01<R>(w1);
-    const R w = R(1) - u01<R>(w2);  // (0, 1]
+    const R w = sizeof(R) == 4 ? (R)(2.0f - u12(w2)) : R(1) - u01<R>(w2);  // (0, 1]
     const R s = fast_sqrt(fmax(R(0), R(1) - z * z));  // f32: v_sqrt_f32 (1 ulp)
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_exp2f(-0.333333343f * __builtin_amdgcn_logf(w));
@@ -559,7 +562,7 @@ template <typename R> __device__ __forceinline__ V<R> unit_ball_inverse(uint32_t
 }
 template <typename R> __device__ __forceinline__ V<R> unit_disk_inverse(uint32_t w0, uint32_t w1) {
     const R turn = u01<R>(w0);
-    const R w = R(1) - u01<R>(w1);  // (0, 1]
+    const R w = sizeof(R) == 4 ? (R)(2.0f - u12(w1)) : R(1) - u01<R>(w1);  // (0, 1]
     if constexpr (sizeof(R) == 4) {
         const float inv_r = __builtin_amdgcn_rsqf(w);
         return mk(inv_r * __builtin_amdgcn_cosf(turn), inv_r * __builtin_amdgcn_sinf(turn), 0.0f);
@@ -3655,8 +3658,13 @@ render_kernel(const RenderParams p, const DSceneView<R> gsc) {
             const uint32_t px = pxy & 0xFFFFu, py = pxy >> 16;
             R ox = R(0), oy = R(0);
             if (p.spp > 1) {
-                ox = u01<R>(w.x) - R(0.5);
-                oy = u01<R>(w.y) - R(0.5);
+                if constexpr (sizeof(R) == 4) {
+                    ox = u12(w.x) - 1.5f;
+                    oy = u12(w.y) - 1.5f;
+                } else {
+                    ox = u01<R>(w.x) - R(0.5);
+                    oy = u01<R>(w.y) - R(0.5);
+                }
             }
             const V<R> point = vfma((R)py + oy, cam(2), vfma((R)px + ox, cam(1), cam(0)));
             if (p.defocus) {
