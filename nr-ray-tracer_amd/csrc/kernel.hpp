@@ -983,12 +983,13 @@ __device__ __forceinline__ uint32_t box_face(const BoxPlanes& b, uint32_t meta, 
     const float fx = fmaxf(b.ax, b.bx), fy = fmaxf(b.ay, b.by), fz = fmaxf(b.az, b.bz);
     const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
     const uint32_t sx = neg_bit(b.ix), sz = 4u | neg_bit(b.iz);
-    uint32_t se = sz, sxit = sz ^ 1u;
-    se = tn == ny ? sy : se;
-    se = tn == nx ? sx : se;
-    sxit = tf == fy ? sy ^ 1u : sxit;
-    sxit = tf == fx ? sx ^ 1u : sxit;
-    const uint32_t slot = entry ? se : sxit;
+    // the plane that gave t (entry: the last near plane, x before y before z on a tie; exit: the
+    // first far plane), then its side: entry slots from the signs, an exit leaves by the other side
+    const float t = entry ? tn : tf, cx = entry ? nx : fx, cy = entry ? ny : fy;
+    uint32_t s = sz;
+    s = t == cy ? sy : s;
+    s = t == cx ? sx : s;
+    const uint32_t slot = entry ? s : s ^ 1u;
     return __builtin_amdgcn_ubfe(meta, WKIND_BITS + 3u * slot, 3);
 }
 // best of a box unit whose face is resolved after the run loop (NRT_BOX_DEFER): the unit's index |
